@@ -1,0 +1,30 @@
+"""Helpers to read the committed golden fixtures (data only; see tests/golden/make_golden.py)."""
+import os
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(tag):
+    z = np.load(os.path.join(GOLDEN, f"{tag}.npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def params(g, prefix="param."):
+    return {k[len(prefix):]: torch.from_numpy(v.copy()) for k, v in g.items() if k.startswith(prefix)}
+
+
+def prepared_input(g):
+    """engine.prepare_data semantics (utils/engine.py:220-245): uint8 [B,T,H,W,3] ->
+    float32 [B,3,T,H,W] / 255 (divide in float64 as numpy does, then cast)."""
+    x = torch.from_numpy(g["clip_u8"].transpose(0, 4, 1, 2, 3) / 255.0).float()
+    y = torch.from_numpy(g["label_u8"].astype(np.float64)).float()
+    return x, y
+
+
+def cfg(g):
+    return dict(cell=str(g["cfg_cell"]), act=str(g["cfg_act"]), no_inh=bool(g["cfg_no_inh"]),
+                lesion=[s for s in str(g["cfg_lesion"]).split(",") if s],
+                dims=int(g["cfg_dims"]))
