@@ -1,0 +1,117 @@
+/*
+ * pt_cell.h — C ABI of the MI355X (gfx950) recurrent-cell library.
+ *
+ * This is the drop-in boundary beneath the reference's model API: the
+ * reference runs InT / hGRU forward as a Python loop of torch ops
+ * (models/InT.py:210-245, cell models/InT.py:145-179;
+ *  models/ffhgru_hierarchy.py:211-276, cell :135-173) and its BPTT backward
+ * through stock autograd (mainclean.py:204).  The Python module
+ * `models/InT.py` of this repo keeps the reference's class / constructor /
+ * forward / state_dict surface and reaches the GPU only through the entry
+ * points below (loaded with ctypes).
+ *
+ * Conventions
+ *  - Plain C types only: device pointers, sizes, an opaque hipStream_t.
+ *  - All tensors are allocated by the caller (PyTorch).  The library keeps no
+ *    allocation and no mutable global state across calls; every call names
+ *    its stream explicitly, so concurrent calls from several host threads
+ *    (the reference's DataParallel replicas) are safe.
+ *  - Return value: 0 on success, non-zero PT_ERR_* on failure; the message is
+ *    available from pt_last_error() (thread-local).
+ *  - Parameters are fp32 device buffers in their PyTorch (state_dict) layout.
+ */
+#ifndef PT_CELL_H
+#define PT_CELL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* pt_stream_t;   /* == hipStream_t */
+
+enum { PT_OK = 0, PT_ERR_ARG = 1, PT_ERR_UNSUPPORTED = 2, PT_ERR_HIP = 3 };
+enum { PT_ACT_SOFTPLUS = 0, PT_ACT_TANH = 1 };      /* the model's `nl` (models/InT.py:184) */
+enum { PT_CELL_INT = 0, PT_CELL_HGRU = 1 };         /* rCell / hConvGRUCell */
+enum { PT_DTYPE_F32 = 0, PT_DTYPE_BF16 = 1 };       /* storage + MFMA operand type */
+
+/* Problem description.  Layout of the input x: [B][3][T][H][W] fp32 (what
+ * engine.prepare_data produces, utils/engine.py:220-255). */
+typedef struct pt_cell_desc {
+    int32_t batch;      /* B  clips on this device                              */
+    int32_t channels;   /* C  = `dimensions` (utils/engine.py:75); must be 32  */
+    int32_t frames;     /* T  = x.shape[2]                                      */
+    int32_t height;     /* H  (32)                                              */
+    int32_t width;      /* W  (32)                                              */
+    int32_t ksize;      /* horizontal kernel size, odd, <= 7 (engine default 7) */
+    int32_t act;        /* PT_ACT_*                                             */
+    int32_t no_inh;     /* InT_no_inh (models/InT.py:168)                       */
+    int32_t cell;       /* PT_CELL_*                                            */
+    int32_t dtype;      /* PT_DTYPE_*                                           */
+    float   eps;        /* BatchNorm eps (1e-3, models/InT.py:102)              */
+} pt_cell_desc;
+
+/* Recurrent-cell parameters, fp32, PyTorch layouts.  Gate order everywhere:
+ * 0 a_w, 1 a_u, 2 i_w, 3 i_u, 4 e_w, 5 e_u (models/InT.py:73-84). */
+typedef struct pt_cell_params {
+    const float* preproc_w;   /* [C,3,1,1,1] */
+    const float* preproc_b;   /* [C]         */
+    const float* w_exc;       /* [C,C,k,k]   */
+    const float* w_inh;       /* [C,C,k,k]   (ignored when no_inh)              */
+    const float* alpha;       /* [C,1,1]     */
+    const float* mu;
+    const float* gamma;
+    const float* kappa;
+    const float* gate_w[6];   /* [C,C,1,1]   */
+    const float* gate_b[6];   /* [C]         */
+    const float* bn_w[2];     /* [C]  bn.0 / bn.1 */
+    const float* bn_b[2];
+} pt_cell_params;
+
+/* Gradient outputs (same shapes as pt_cell_params; fp32, overwritten).  Any
+ * pointer may be NULL when the caller does not want that gradient. */
+typedef struct pt_cell_grads {
+    float* preproc_w; float* preproc_b;
+    float* w_exc; float* w_inh;
+    float* alpha; float* mu; float* gamma; float* kappa;
+    float* gate_w[6]; float* gate_b[6];
+    float* bn_w[2]; float* bn_b[2];
+} pt_cell_grads;
+
+/* Bytes the caller must keep alive from pt_cell_forward to pt_cell_backward
+ * (per-frame states and conv pre-activations, BN statistics, prepared weight
+ * fragments), and bytes of transient workspace (reusable between calls). */
+size_t pt_cell_saved_bytes(const pt_cell_desc* d);
+size_t pt_cell_workspace_bytes(const pt_cell_desc* d);
+
+/* Forward over all T frames (replaces the frame loop models/InT.py:223-235).
+ *   x       [B,3,T,H,W] fp32
+ *   e_last  [B,C,H,W] fp32 out: the excitation after the last frame (input of
+ *           the readout, models/InT.py:236)
+ *   gates   [B,T,C,H,W] fp32 out or NULL: attention maps (testmode, :230-233)
+ */
+int pt_cell_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* p,
+                    void* saved, void* workspace, float* e_last, float* gates,
+                    pt_stream_t stream);
+
+/* Per-frame excitations E_t, t = 0..T-1, as [B,T,C,H,W] fp32 (testmode
+ * `states` are readout_conv of these, models/InT.py:233). */
+int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq,
+                       pt_stream_t stream);
+
+/* BPTT backward (replaces autograd through the frame loop).
+ *   d_e_last  [B,C,H,W] fp32: dLoss/d e_last from the readout.
+ * Writes every parameter gradient (overwrite, not accumulate). */
+int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* p,
+                     const void* saved, void* workspace, const float* d_e_last,
+                     const pt_cell_grads* g, pt_stream_t stream);
+
+const char* pt_last_error(void);
+const char* pt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_CELL_H */

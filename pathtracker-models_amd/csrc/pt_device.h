@@ -1,0 +1,276 @@
+// pt_device.h — gfx950 device building blocks for the recurrent-cell kernels.
+//
+// Register layouts used throughout (one wave = one 32-pixel image row):
+//
+//  CL ("channel on lane")  the C/D layout of a 32x32 MFMA tile whose rows are
+//      the 32 pixels of a row and whose columns are the 32 channels:
+//        lane l -> channel c = l & 31, half h = l >> 5
+//        reg  r -> pixel   x = (r & 3) + 8 (r >> 2) + 4 h
+//      Every per-pixel tensor lives in this layout (f32x16 per lane), so
+//      per-channel parameters are ONE register per lane and BatchNorm sums are
+//      lane-local.
+//
+//  PA ("pixel on A")  the A-operand layout of the same tile: lane l holds
+//      pixel p = l & 31 and, at k-step s, the channels frag_chan<S>(s, h, j).
+//      Needed where a 1x1 conv contracts over channels; produced from CL by a
+//      per-wave LDS transpose (cl_to_pa).
+//
+// MFMA flavours (storage type S):
+//   S = float  : v_mfma_f32_32x32x2_f32   (exact f32, parity path; 16 k-steps / 32 ch)
+//   S = __bf16 : v_mfma_f32_32x32x16_bf16 (f32 accumulate; 2 k-steps / 32 ch)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptc {
+
+constexpr int C = 32;          // channels (MFMA tile width)
+constexpr int IMG = 32;        // H = W = 32
+constexpr int NPIX = IMG * IMG;
+constexpr int PADMAX = 3;      // halo for k <= 7
+constexpr int TILE = IMG + 2 * PADMAX;   // 38
+constexpr int NT = 256;        // threads per block
+constexpr int NWAVE = NT / 64;
+constexpr int RPW = IMG / NWAVE;         // image rows per wave (8)
+constexpr int MAXTAP = 49;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16_t;
+
+template <class S> struct Tr;
+template <> struct Tr<float> {
+  using frag = float;
+  static constexpr int KS = 16;     // k-steps per 32-channel contraction
+  static constexpr int EPL = 1;     // fragment elements per lane
+  static constexpr int CP = 16;     // channels per conv pass held in LDS
+  static constexpr int NPASS = 2;
+  __device__ static inline f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Tr<bf16_t> {
+  using frag = bf16x8;
+  static constexpr int KS = 2;
+  static constexpr int EPL = 8;
+  static constexpr int CP = 32;
+  static constexpr int NPASS = 1;
+  __device__ static inline f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+// Channel carried by element j of a lane in half h at k-step s.
+template <class S> __host__ __device__ constexpr int frag_chan(int s, int h, int j);
+template <> __host__ __device__ constexpr int frag_chan<float>(int s, int h, int) { return 2 * s + h; }
+template <> __host__ __device__ constexpr int frag_chan<bf16_t>(int s, int h, int j) {
+  return 16 * s + 8 * h + j;
+}
+
+__device__ __forceinline__ int cl_x(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ float ldf(const float* p) { return *p; }
+__device__ __forceinline__ float ldf(const bf16_t* p) { return (float)*p; }
+__device__ __forceinline__ void stf(float* p, float v) { *p = v; }
+__device__ __forceinline__ void stf(bf16_t* p, float v) { *p = (bf16_t)v; }
+
+// Load / store one CL row tile from a channels-last [32 px][32 ch] row.
+template <class S>
+__device__ __forceinline__ f32x16 load_cl(const S* __restrict__ row, int c, int h) {
+  f32x16 v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = ldf(row + cl_x(r, h) * C + c);
+  return v;
+}
+template <class S>
+__device__ __forceinline__ void store_cl(S* __restrict__ row, int c, int h, const f32x16& v) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) stf(row + cl_x(r, h) * C + c, v[r]);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = 0.f;
+  return v;
+}
+
+// Consume per-row accumulators in a non-unrolled row loop without dynamic
+// register indexing (which LLVM would lower to scratch): use a[0], then shift.
+template <int N>
+__device__ __forceinline__ void shift_rows(f32x16 (&a)[N]) {
+#pragma unroll
+  for (int k = 0; k + 1 < N; ++k) a[k] = a[k + 1];
+}
+
+__device__ __forceinline__ float hsum16(const f32x16& v) {
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += v[r];
+  return s;
+}
+
+// ---------------------------------------------------------------- activations
+// nl = softplus(beta=1, threshold=20) or tanh (models/InT.py:184, engine.py:145)
+__device__ __forceinline__ float act_f(float x, int act) {
+  if (act == 0) return x > 20.f ? x : log1pf(expf(x));
+  return tanhf(x);
+}
+__device__ __forceinline__ float act_d(float x, int act) {   // d nl / d x
+  if (act == 0) return x > 20.f ? 1.f : 1.f / (1.f + expf(-x));
+  const float t = tanhf(x);
+  return 1.f - t * t;
+}
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+// --------------------------------------------------------- per-wave transpose
+// 32x32 f32 scratch, swizzled so the CL write and the PA read are both
+// bank-conflict free for the read width each dtype uses.
+template <class S> __device__ __forceinline__ int scr_idx(int p, int c);
+template <> __device__ __forceinline__ int scr_idx<float>(int p, int c) { return p * 32 + (c ^ p); }
+template <> __device__ __forceinline__ int scr_idx<bf16_t>(int p, int c) {
+  return p * 32 + ((((c >> 2) ^ ((p >> 1) & 7))) << 2) + (c & 3);
+}
+
+__device__ __forceinline__ void wave_sync() {
+  // DS instructions of one wave execute in order; this only pins the compiler.
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <class S>
+__device__ __forceinline__ void cl_to_pa(float* __restrict__ scr, const f32x16& v, int lane,
+                                         typename Tr<S>::frag (&pa)[Tr<S>::KS]) {
+  const int c = lane & 31, h = lane >> 5, p = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) scr[scr_idx<S>(cl_x(r, h), c)] = v[r];
+  wave_sync();
+  if constexpr (sizeof(S) == 4) {
+#pragma unroll
+    for (int s = 0; s < Tr<S>::KS; ++s) pa[s] = scr[scr_idx<float>(p, 2 * s + h)];
+  } else {
+#pragma unroll
+    for (int s = 0; s < Tr<S>::KS; ++s) {
+      const int q0 = 4 * s + 2 * h;
+      const f32x4 lo = *(const f32x4*)(scr + p * 32 + ((q0 ^ ((p >> 1) & 7)) << 2));
+      const f32x4 hi = *(const f32x4*)(scr + p * 32 + (((q0 + 1) ^ ((p >> 1) & 7)) << 2));
+      bf16x8 f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { f[j] = (bf16_t)lo[j]; f[4 + j] = (bf16_t)hi[j]; }
+      pa[s] = f;
+    }
+  }
+  wave_sync();
+}
+
+// Y[p][n] += sum_c X[p][c] G[n][c]; X in PA, G as prepared B fragments [KS][64].
+template <class S>
+__device__ __forceinline__ f32x16 gemm_pa(const typename Tr<S>::frag (&pa)[Tr<S>::KS],
+                                          const typename Tr<S>::frag* __restrict__ g, f32x16 acc,
+                                          int lane) {
+#pragma unroll
+  for (int s = 0; s < Tr<S>::KS; ++s) acc = Tr<S>::mma(pa[s], g[s * 64 + lane], acc);
+  return acc;
+}
+
+// dW[n][ci] += sum_p D[p][n] X[p][ci] with D, X both in CL registers: the
+// accumulator tiles are used directly as A (= D^T) and B operands; the k
+// (pixel) order is the same permutation on both sides.
+template <class S>
+__device__ __forceinline__ f32x16 wgrad_cl(const f32x16& d, const f32x16& x, f32x16 acc) {
+  if constexpr (sizeof(S) == 4) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = Tr<float>::mma(d[s], x[s], acc);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 fa, fb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { fa[j] = (bf16_t)d[8 * s + j]; fb[j] = (bf16_t)x[8 * s + j]; }
+      acc = Tr<bf16_t>::mma(fa, fb, acc);
+    }
+  }
+  return acc;
+}
+
+// -------------------------------------------------------------- conv LDS tile
+// [TILE rows][TILE cols][CP channels] of S, zero halo.  bf16: 16-B chunks of
+// 8 channels XOR-swizzled by (col >> 2) & 3 so the 32 lanes of an A-fragment
+// read (consecutive columns, same chunk) hit distinct bank groups.
+template <class S> __device__ __forceinline__ int tile_off(int trow, int tcol, int ch);
+template <> __device__ __forceinline__ int tile_off<float>(int trow, int tcol, int ch) {
+  return (trow * TILE + tcol) * Tr<float>::CP + ch;
+}
+template <> __device__ __forceinline__ int tile_off<bf16_t>(int trow, int tcol, int ch) {
+  return (trow * TILE + tcol) * 32 + ((((ch >> 3) ^ ((tcol >> 2) & 3))) << 3) + (ch & 7);
+}
+template <class S>
+__host__ __device__ constexpr int tile_bytes() {
+  return TILE * TILE * Tr<S>::CP * (int)sizeof(S);
+}
+
+template <class S>
+__device__ void tile_zero(S* tile, int tid) {
+  uint4* p = (uint4*)tile;
+  const int n = tile_bytes<S>() / 16;
+  for (int i = tid; i < n; i += NT) p[i] = make_uint4(0, 0, 0, 0);
+}
+
+// Fill the tile interior with channels [pass*CP, pass*CP+CP) of a
+// channels-last clip image (global, [32][32][32] of S).
+template <class S>
+__device__ void tile_fill(S* __restrict__ tile, const S* __restrict__ src, int pass, int tid) {
+  constexpr int CPB = 16 / (int)sizeof(S);          // channels per 16-B chunk
+  constexpr int NCH = Tr<S>::CP / CPB;               // chunks per pixel
+  for (int idx = tid; idx < NPIX * NCH; idx += NT) {
+    const int pix = idx / NCH, q = idx % NCH;
+    const int y = pix >> 5, x = pix & 31;
+    const uint4 v = *(const uint4*)(src + pix * C + pass * Tr<S>::CP + q * CPB);
+    *(uint4*)(tile + tile_off<S>(y + PADMAX, x + PADMAX, q * CPB)) = v;
+  }
+}
+
+// Implicit-GEMM k x k conv over the LDS tile for this wave's RPW rows:
+//   acc[i][x][n] += sum_{tap,ci} in[row0+i+kh-pad][x+kw-pad][ci] * W[n][ci][tap]
+// wf: B fragments [K*K][KS][64] (prepared by k_prep).  The caller has zeroed
+// the tile halo; this routine refills the interior per pass.
+template <class S>
+__device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], const S* __restrict__ src,
+                         const typename Tr<S>::frag* __restrict__ wf, S* tile, int K, int row0,
+                         int tid, int lane) {
+  using TT = Tr<S>;
+  constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
+  const int off = PADMAX - K / 2;
+  const int h = lane >> 5, px = lane & 31;
+  for (int pass = 0; pass < TT::NPASS; ++pass) {
+    __syncthreads();
+    tile_fill<S>(tile, src, pass, tid);
+    __syncthreads();
+    for (int kh = 0; kh < K; ++kh) {
+      for (int kw = 0; kw < K; ++kw) {
+        const int tap = kh * K + kw;
+        const int tcol = px + kw + off;
+#pragma unroll
+        for (int s = 0; s < KSP; ++s) {
+          const int ks = pass * KSP + s;
+          const typename TT::frag b = wf[(tap * TT::KS + ks) * 64 + lane];
+#pragma unroll
+          for (int i = 0; i < RPW; ++i) {
+            const int trow = row0 + i + kh + off;
+            typename TT::frag a;
+            if constexpr (sizeof(S) == 4) {
+              a = tile[tile_off<S>(trow, tcol, 2 * s + h)];
+            } else {
+              a = *(const bf16x8*)(tile + tile_off<S>(trow, tcol, 16 * s + 8 * h));
+            }
+            acc[i] = TT::mma(a, b, acc[i]);
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace ptc

@@ -1,0 +1,86 @@
+"""ctypes binding of the C-ABI library ``libptcell.so`` (include/pt_cell.h).
+
+The shared library is built in-tree (``__graft_entry__.build()`` or
+``python -m ptamd.build``) next to this file.  There is no fallback: if the
+library or a ROCm device is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libptcell.so")
+
+PT_ACT_SOFTPLUS, PT_ACT_TANH = 0, 1
+PT_CELL_INT, PT_CELL_HGRU = 0, 1
+PT_DTYPE_F32, PT_DTYPE_BF16 = 0, 1
+
+# Exported symbols declared in include/pt_cell.h (tests check all are present).
+EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
+           "pt_cell_export_exc", "pt_cell_backward", "pt_last_error", "pt_version")
+
+_P = ctypes.c_void_p
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32),
+                ("frames", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("ksize", ctypes.c_int32),
+                ("act", ctypes.c_int32), ("no_inh", ctypes.c_int32),
+                ("cell", ctypes.c_int32), ("dtype", ctypes.c_int32),
+                ("eps", ctypes.c_float)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("preproc_w", _P), ("preproc_b", _P), ("w_exc", _P), ("w_inh", _P),
+                ("alpha", _P), ("mu", _P), ("gamma", _P), ("kappa", _P),
+                ("gate_w", _P * 6), ("gate_b", _P * 6), ("bn_w", _P * 2), ("bn_b", _P * 2)]
+
+
+class Grads(ctypes.Structure):
+    _fields_ = Params._fields_
+
+
+class PtCellError(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load():
+    """Load (once) and return the library; raise if it is not built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise PtCellError(
+                f"{LIB_PATH} is missing: build the HIP extension first "
+                "(python __graft_entry__.py build, or python -m ptamd.build)")
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.pt_cell_saved_bytes.restype = ctypes.c_size_t
+        lib.pt_cell_saved_bytes.argtypes = [ctypes.POINTER(Desc)]
+        lib.pt_cell_workspace_bytes.restype = ctypes.c_size_t
+        lib.pt_cell_workspace_bytes.argtypes = [ctypes.POINTER(Desc)]
+        lib.pt_cell_forward.restype = ctypes.c_int
+        lib.pt_cell_forward.argtypes = [ctypes.POINTER(Desc), _P, ctypes.POINTER(Params), _P, _P,
+                                        _P, _P, _P]
+        lib.pt_cell_export_exc.restype = ctypes.c_int
+        lib.pt_cell_export_exc.argtypes = [ctypes.POINTER(Desc), _P, _P, _P]
+        lib.pt_cell_backward.restype = ctypes.c_int
+        lib.pt_cell_backward.argtypes = [ctypes.POINTER(Desc), _P, ctypes.POINTER(Params), _P, _P,
+                                         _P, ctypes.POINTER(Grads), _P]
+        lib.pt_last_error.restype = ctypes.c_char_p
+        lib.pt_version.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().pt_last_error().decode(errors="replace")
+        raise PtCellError(f"pt_cell error {rc}: {msg}")

@@ -1,0 +1,152 @@
+"""Autograd bridge: the whole-clip recurrent cell as one ``torch.autograd.Function``.
+
+Forward and backward are single calls into the C-ABI HIP library
+(``include/pt_cell.h``): torch owns every buffer (inputs, outputs, the saved
+state blob, the workspace) and the library sees raw device pointers and the
+current HIP stream.  This replaces, for the reference's InT
+(models/InT.py:210-245), the Python frame loop (:223-235) and the autograd
+BPTT through it (mainclean.py:204).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+# Parameter order handed to the Function (names are the reference state_dict keys).
+GATES = ("a_w", "a_u", "i_w", "i_u", "e_w", "e_u")
+PARAM_KEYS = (["preproc.weight", "preproc.bias", "unit1.w_exc", "unit1.w_inh",
+               "unit1.alpha", "unit1.mu", "unit1.gamma", "unit1.kappa"]
+              + [f"unit1.{g}_gate.weight" for g in GATES]
+              + [f"unit1.{g}_gate.bias" for g in GATES]
+              + ["unit1.bn.0.weight", "unit1.bn.1.weight", "unit1.bn.0.bias", "unit1.bn.1.bias"])
+
+DTYPES = {"f32": _lib.PT_DTYPE_F32, "fp32": _lib.PT_DTYPE_F32, "float32": _lib.PT_DTYPE_F32,
+          "bf16": _lib.PT_DTYPE_BF16, "bfloat16": _lib.PT_DTYPE_BF16}
+
+
+@dataclass(frozen=True)
+class CellConfig:
+    ksize: int = 7
+    act: str = "softplus"        # 'softplus' | 'tanh'
+    no_inh: bool = False
+    cell: str = "int"            # 'int' (rCell) | 'hgru' (hConvGRUCell)
+    dtype: str = "f32"           # 'f32' (parity) | 'bf16' (throughput)
+    eps: float = 1e-3
+
+
+# Parameters the no_inh branch never reads (models/InT.py:168): the reference
+# leaves their .grad None, so must we.
+_UNUSED_NO_INH = {"unit1.w_inh", "unit1.alpha", "unit1.mu", "unit1.i_w_gate.weight",
+                  "unit1.i_u_gate.weight", "unit1.i_w_gate.bias", "unit1.i_u_gate.bias",
+                  "unit1.bn.0.weight", "unit1.bn.0.bias"}
+
+
+def _desc(cfg: CellConfig, x: torch.Tensor, channels: int) -> _lib.Desc:
+    b, _, t, h, w = x.shape
+    return _lib.Desc(batch=b, channels=channels, frames=t, height=h, width=w, ksize=cfg.ksize,
+                     act=_lib.PT_ACT_TANH if cfg.act == "tanh" else _lib.PT_ACT_SOFTPLUS,
+                     no_inh=int(cfg.no_inh),
+                     cell=_lib.PT_CELL_HGRU if cfg.cell == "hgru" else _lib.PT_CELL_INT,
+                     dtype=DTYPES[cfg.dtype], eps=cfg.eps)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _pack(struct_cls, tensors):
+    """Fill a Params/Grads struct from tensors in PARAM_KEYS order (None -> NULL)."""
+    s = struct_cls()
+    vals = [t.data_ptr() if t is not None else 0 for t in tensors]
+    (s.preproc_w, s.preproc_b, s.w_exc, s.w_inh, s.alpha, s.mu, s.gamma, s.kappa) = vals[:8]
+    for i in range(6):
+        s.gate_w[i] = vals[8 + i]
+        s.gate_b[i] = vals[14 + i]
+    s.bn_w[0], s.bn_w[1], s.bn_b[0], s.bn_b[1] = vals[20:24]
+    return s
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_device(x):
+    if x.device.type != "cuda":
+        raise RuntimeError("the InT HIP cell runs on a ROCm device only (got a "
+                           f"{x.device.type} tensor); there is no CPU fallback")
+
+
+class RecurrentCellFn(torch.autograd.Function):
+    """(x [B,3,T,H,W], params...) -> (E_T [B,C,H,W], E_seq [B,T,C,H,W], att [B,T,C,H,W]).
+
+    E_seq / att are only filled when ``want_seq`` (testmode); otherwise they
+    are empty tensors.  Only E_T is differentiable.
+    """
+
+    @staticmethod
+    def forward(ctx, x, cfg: CellConfig, want_seq: bool, *params):
+        _require_device(x)
+        lib = _lib.load()
+        x = x.contiguous().float()
+        params = [p.contiguous().float() if p is not None else None for p in params]
+        c = params[0].shape[0]
+        d = _desc(cfg, x, c)
+        saved = torch.empty(lib.pt_cell_saved_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                            device=x.device)
+        if saved.numel() == 0:
+            _lib.check(1)
+        ws = torch.empty(lib.pt_cell_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                         device=x.device)
+        b, _, t, h, w = x.shape
+        e_last = torch.empty((b, c, h, w), dtype=torch.float32, device=x.device)
+        gates = torch.empty((b, t, c, h, w) if want_seq else (0,), dtype=torch.float32,
+                            device=x.device)
+        pp = _pack(_lib.Params, params)
+        st = _stream(x.device)
+        _lib.check(lib.pt_cell_forward(ctypes.byref(d), _ptr(x), ctypes.byref(pp), _ptr(saved),
+                                       _ptr(ws), _ptr(e_last), _ptr(gates) if want_seq else None,
+                                       st))
+        e_seq = torch.empty((b, t, c, h, w) if want_seq else (0,), dtype=torch.float32,
+                            device=x.device)
+        if want_seq:
+            _lib.check(lib.pt_cell_export_exc(ctypes.byref(d), _ptr(saved), _ptr(e_seq), st))
+        ctx.cfg = cfg
+        ctx.saved_blob = saved
+        ctx.save_for_backward(x, *[p if p is not None else torch.empty(0) for p in params])
+        ctx.has = [p is not None for p in params]
+        ctx.mark_non_differentiable(e_seq, gates)
+        return e_last, e_seq, gates
+
+    @staticmethod
+    def backward(ctx, d_e_last, _d_seq, _d_gates):
+        lib = _lib.load()
+        x, *params = ctx.saved_tensors
+        params = [p if has else None for p, has in zip(params, ctx.has)]
+        c = params[0].shape[0]
+        d = _desc(ctx.cfg, x, c)
+        if d_e_last is None:
+            d_e_last = torch.zeros((x.shape[0], c, x.shape[3], x.shape[4]), device=x.device)
+        d_e_last = d_e_last.contiguous().float()
+        ws = torch.empty(lib.pt_cell_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                         device=x.device)
+        need = list(ctx.needs_input_grad[3:])
+        if ctx.cfg.no_inh:
+            need = [n and PARAM_KEYS[i] not in _UNUSED_NO_INH for i, n in enumerate(need)]
+        grads = [torch.empty_like(p) if (p is not None and need[i]) else None
+                 for i, p in enumerate(params)]
+        pp = _pack(_lib.Params, params)
+        gg = _pack(_lib.Grads, grads)
+        _lib.check(lib.pt_cell_backward(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
+                                        _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_e_last),
+                                        ctypes.byref(gg), _stream(x.device)))
+        ctx.saved_blob = None
+        return (None, None, None, *grads)
+
+
+def run_cell(x, params, cfg: CellConfig, want_seq: bool = False):
+    """Apply the HIP recurrent cell.  ``params`` is a list in PARAM_KEYS order."""
+    return RecurrentCellFn.apply(x, cfg, want_seq, *params)

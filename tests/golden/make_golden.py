@@ -184,6 +184,16 @@ def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0):
     print(tag, "loss", float(out["loss"]))
 
 
+def make_init(ref_int, tag, seed=123):
+    """Initial parameters under a fixed seed (RNG-order parity of the drop-in)."""
+    torch.manual_seed(seed)
+    model = ref_int.InT(dimensions=32, timesteps=8, kernel_size=7, jacobian_penalty=False,
+                        grad_method="bptt")
+    sd = {k: v.numpy() for k, v in model.state_dict().items() if k != "unit1.w"}  # torch.empty
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **sd)
+    print(tag, len(sd), "tensors")
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not mounted; golden vectors are generated in the build container only")
@@ -198,6 +208,9 @@ def main():
         ref_hgru = _load("ref_ffhgru", os.path.join(REF, "models", "ffhgru_hierarchy.py"))
         ref_clstm = _load("ref_convlstm", os.path.join(REF, "models", "convlstm.py"))
 
+        make_init(ref_int, "init_seed123")
+        if os.environ.get("GOLDEN_ONLY_INIT"):
+            return
         make_int(ref_int, "int_tiny_c8", batch=2, t_len=8, dims=8)
         make_int(ref_int, "int_c32", batch=2, t_len=8, dims=32, seed=1)
         make_int(ref_int, "int_noinh", batch=2, t_len=8, dims=32, no_inh=True, seed=2)

@@ -1,0 +1,94 @@
+"""CPU-only checks of the product boundary (no GPU calls).
+
+* the C-ABI library loads and exports every symbol include/pt_cell.h declares;
+* size queries (pure host code) behave and reject unsupported shapes;
+* the drop-in model keeps the reference's state_dict keys / shapes / order,
+  its initial values (same RNG order; pinned by tests/golden/init_*.npz) and
+  refuses to run off-GPU instead of falling back to a CPU path.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from goldens import GOLDEN, load
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(REPO, "include", "pt_cell.h")).read()
+    return sorted(set(re.findall(r"\b(pt_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    from ptamd import _lib
+    assert sorted(_lib.EXPORTS) == _header_symbols()
+
+
+def test_library_exports_every_symbol():
+    from ptamd import _lib
+    lib = _lib.load()
+    for sym in _header_symbols():
+        assert hasattr(lib, sym), sym
+    assert lib.pt_version().decode().startswith("pt_cell")
+
+
+def test_size_queries_and_validation():
+    from ptamd import _lib
+    lib = _lib.load()
+    d = _lib.Desc(batch=256, channels=32, frames=64, height=32, width=32, ksize=7, act=0,
+                  no_inh=0, cell=0, dtype=_lib.PT_DTYPE_BF16, eps=1e-3)
+    saved = lib.pt_cell_saved_bytes(ctypes.byref(d))
+    frame = 256 * 1024 * 32 * 2
+    assert saved >= 6 * 64 * frame          # six per-frame tensors kept for BPTT
+    assert lib.pt_cell_workspace_bytes(ctypes.byref(d)) >= 2 * 64 * frame
+    bad = _lib.Desc(batch=2, channels=16, frames=8, height=32, width=32, ksize=7, act=0,
+                    no_inh=0, cell=0, dtype=0, eps=1e-3)
+    assert lib.pt_cell_saved_bytes(ctypes.byref(bad)) == 0
+    assert b"channels" in lib.pt_last_error()
+    bad.channels, bad.ksize = 32, 4
+    assert lib.pt_cell_saved_bytes(ctypes.byref(bad)) == 0
+
+
+@pytest.mark.parametrize("tag", ["int_c32", "int_noinh", "int_lesion"])
+def test_state_dict_keys_match_reference(tag):
+    from models import InT as int_mod
+    g = load(tag)
+    ref_keys = [k[len("param."):] for k in g if k.startswith("param.")]
+    kw = dict(dimensions=32, timesteps=8, kernel_size=7, no_inh=bool(g["cfg_no_inh"]))
+    m = int_mod.InT(**kw)
+    sd = m.state_dict()
+    assert list(sd) == ref_keys            # same keys, same order
+    for k in ref_keys:
+        assert tuple(sd[k].shape) == g["param." + k].shape, k
+
+
+def test_init_matches_reference_rng_order():
+    from models import InT as int_mod
+    path = os.path.join(GOLDEN, "init_seed123.npz")
+    if not os.path.exists(path):
+        pytest.skip("init fixture not generated")
+    z = np.load(path, allow_pickle=False)
+    torch.manual_seed(123)
+    m = int_mod.InT(dimensions=32, timesteps=8, kernel_size=7)
+    sd = m.state_dict()
+    for k in z.files:
+        np.testing.assert_array_equal(sd[k].numpy(), z[k], err_msg=k)
+
+
+def test_lesion_freezes_only_named_params():
+    from models import InT as int_mod
+    m = int_mod.InT(dimensions=32, kernel_size=7, lesion_alpha=True, lesion_gamma=True)
+    frozen = {n for n, p in m.named_parameters() if not p.requires_grad}
+    assert frozen == {"unit1.alpha", "unit1.gamma"}
+
+
+def test_no_cpu_fallback():
+    from models import InT as int_mod
+    m = int_mod.InT(dimensions=32, timesteps=4, kernel_size=7)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        m(torch.rand(1, 3, 4, 32, 32))
