@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""bench.py — InT training throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): InT, 32x32 frames x 64, C=32, k=7,
+B=256 clips per GPU, bf16 cell (bf16 operands / saved states, f32 accumulate),
+one step = forward over all frames + readout + BCE loss + BPTT backward
+[+ one RCCL all-reduce of the flat gradient bucket when N>1] + Adam step.
+Synthetic seeded PathTracker clips (ptamd.synth), resident in HBM before the
+timed region; random init (no checkpoints offline).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+N>1 is launched by torch.distributed.run (one rank per GPU, RCCL); rank 0
+prints ONE JSON line.  value = clips/s of the whole job (all ranks) =
+N * B * K / max-over-ranks(time of K steps).  Scaling is weak (B fixed per GPU).
+
+roofline: the dominant kernel (largest summed device time inside the timed
+region, measured with HIP events the library records around its own launches
+on the launch stream) against the dense bf16 MFMA peak, with algorithmic
+FLOPs per launch from DESIGN.md §4.  cpu_baseline: the CPU oracle
+(oracle/cells.py, plain PyTorch fp32, the reference's own op graph) timed on
+this host for a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "pathtracker-models_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+C, HW, K = 32, 32, 7
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}     # dense MFMA peaks, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def conv_flops():          # one k x k C->C conv over one 32x32 clip frame
+    return 2 * C * C * K * K * HW * HW
+
+
+def gate_flops():          # one 1x1 C->C gate conv over one clip frame
+    return 2 * C * C * HW * HW
+
+
+def algorithmic_flops(kind, batch, frames):
+    """Algorithmic FLOPs of ALL launches of one kernel kind in one step.
+
+    Counts the model's contractions only (no recompute): forward conv + gates;
+    backward data-gradients + 1x1 weight-gradients; the k x k weight gradients
+    in k_wgrad.  Sum over kinds = 3 x forward = SURVEY.md §8(d)'s 41.9 GFLOP/clip
+    at T=64 (minus the stem's 12.6 MFLOP, counted nowhere)."""
+    cf, gf = conv_flops(), gate_flops()
+    per_clip = {
+        "k_fwd_a": frames * (cf + 4 * gf),          # conv(gE,w_inh) + a_w,a_u,e_w,e_u
+        "k_fwd_b": frames * (cf + 2 * gf),          # conv(I,w_exc) + i_w,i_u
+        "k_bwd_a": (frames - 1) * (cf + 4 * gf)     # conv^T(w_inh) + a_* dgrad/wgrad
+                   + frames * 0,
+        "k_bwd_b": frames * (cf + 8 * gf),          # conv^T(w_exc) + i_*,e_* dgrad/wgrad
+        "k_wgrad": frames * 2 * cf,                 # dW_inh + dW_exc
+    }.get(kind, 0)
+    return per_clip * batch
+
+
+def make_data(seed, batch, frames, device):
+    from ptamd import synth
+    clips, labels = synth.make_batch(seed, batch, frames)
+    x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3).astype(np.float32) / 255.0)
+    y = torch.tensor([ord(b) for b in labels], dtype=torch.float32)
+    return x.to(device), y.to(device)
+
+
+def cpu_baseline(seconds, frames=64, batch=4):
+    """Oracle (reference op graph, fp32 CPU) fwd+BPTT+Adam on B=4 clips."""
+    from oracle import cells
+    from ptamd import synth
+    torch.manual_seed(0)
+    from models import InT as int_mod
+    m = int_mod.InT(dimensions=C, timesteps=frames, kernel_size=K)
+    sd = {k: v.detach().clone().requires_grad_(k != "unit1.w") for k, v in m.state_dict().items()}
+    clips, labels = synth.make_batch(99, batch, frames)
+    x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float()
+    y = torch.tensor([ord(b) for b in labels], dtype=torch.float32)
+    opt = torch.optim.Adam([v for v in sd.values() if v.requires_grad], lr=3e-4)
+
+    def step():
+        logits, _, _ = cells.recurrent_forward(sd, x)
+        cells.bce_logits(logits, y).backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    step()                                   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    return {"value": round(batch * n / el, 3), "unit": "clips/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/cells.py InT fwd+BPTT+Adam, B={batch} T={frames} 32x32 fp32, "
+                      f"{n} steps in {el:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="clips per GPU")
+    ap.add_argument("--frames", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from ptamd import _lib
+    from ptamd.dist import GradBucket, env_rank
+    from models import InT as int_mod
+
+    rank, local_rank, world = env_rank()
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    torch.manual_seed(1234)
+    model = int_mod.InT(dimensions=C, timesteps=args.frames, kernel_size=K).to(dev)
+    model.cell_dtype = args.dtype
+    if world > 1:                       # identical init on every rank
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    bucket = GradBucket(model.parameters(), dev)
+    opt = torch.optim.Adam(model.parameters(), lr=3e-4)
+    crit = torch.nn.BCEWithLogitsLoss()
+    x, y = make_data(1000 + rank, args.batch, args.frames, dev)
+
+    def step():
+        out, _ = model(x)
+        loss = crit(out, y.reshape(-1, 1))
+        loss.backward()
+        bucket.allreduce_mean()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib = _lib.load()
+    lib.pt_cell_timing_reset()
+    lib.pt_cell_timing_enable((1 << 7) - 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    lib.pt_cell_timing_enable(0)
+    kern = {}
+    for kind, name in enumerate(_lib.KIND_NAMES):
+        ms, n = _lib.timing_read(kind)
+        kern[name] = (ms, n)
+    lib.pt_cell_timing_reset()
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    if rank == 0:
+        value = world * args.batch * args.steps / el
+        dom = max(kern, key=lambda k: kern[k][0])
+        dom_ms, dom_n = kern[dom]
+        flops_step = algorithmic_flops(dom, args.batch, args.frames)
+        avg_ms = dom_ms / max(dom_n, 1)
+        per_launch = flops_step * args.steps / max(dom_n, 1)
+        achieved = per_launch / (avg_ms * 1e-3) / 1e12
+        peak = PEAK_TFLOPS[args.dtype]
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "clips/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic",
+            "config": {"workload": f"InT 32x32x{args.frames}f fwd+BPTT+Adam, "
+                                   f"{args.batch} clips/GPU, {args.dtype} cell",
+                       "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "frames": args.frames, "channels": C, "kernel": K,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2),
+                         "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                         "traffic": None, "avg_launch_ms": round(avg_ms, 4),
+                         "launches": dom_n, "algorithmic_flop_per_launch": int(per_launch)},
+            "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
+            "loss": round(float(loss.item()), 5),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, frames=args.frames)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

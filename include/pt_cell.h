@@ -108,6 +108,18 @@ int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params
                      const void* saved, void* workspace, const float* d_e_last,
                      const pt_cell_grads* g, pt_stream_t stream);
 
+/* Optional kernel timing for benchmarks (process-wide, off by default; the
+ * only mutable library state, guarded by a mutex).  When enabled for a kernel
+ * kind, every launch of that kind is bracketed by two hipEvents on its launch
+ * stream.  Reading
+ * synchronises on the recorded events and returns the summed device time and
+ * the launch count since the last reset.  Kinds: */
+enum { PT_K_FWD_A = 0, PT_K_FWD_B = 1, PT_K_BWD_A = 2, PT_K_BWD_B = 3, PT_K_WGRAD = 4,
+       PT_K_PREP = 5, PT_K_REDUCE = 6, PT_K_NKINDS = 7 };
+int pt_cell_timing_enable(uint32_t kind_mask);      /* bit k enables kind k; 0 disables */
+int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches);
+int pt_cell_timing_reset(void);
+
 const char* pt_last_error(void);
 const char* pt_version(void);
 

@@ -20,6 +20,8 @@
 
 #include <stdio.h>
 #include <string.h>
+#include <mutex>
+#include <vector>
 
 namespace ptc {
 
@@ -76,13 +78,13 @@ struct CellArgs {
   const F* gt[6];                       // 1x1 fragments, transposed (backward)
   S *E, *I, *gE, *ci, *ce, *eg;         // saved per frame [T][B][32][32][32]
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
-  float2 *part0, *part1;                // fwd BN partials [B][32] (mean, M2)
+  double* bnacc;                        // fwd BN sums [T][2][3][32]: sum mean_b, sum mean_b^2, sum M2_b
   float* gates;                         // [B][T][C][32][32] or null
   // backward
   float *dEn, *dcE, *dIl, *dEp, *dcI, *GI, *dgEp, *dxp;   // f32 [B][32][32][32]
   const float* GEfin;                   // f32 channels-last dE of the last frame
   S *dci_s, *dce_s;                     // [T][B][32][32][32] conv-output grads (for k_wgrad)
-  float2 *bpart0, *bpart1;              // bwd BN partials [B][32] (sum dy, sum dy*xhat)
+  double* bnbacc;                       // bwd BN sums [T][2][2][32]: sum dy, sum dy*xhat
   float* slab;                          // [B][SLAB]
 };
 
@@ -113,63 +115,37 @@ __device__ __forceinline__ void stem_cl(const f32x4* xs, int y, int h, const Ste
   }
 }
 
-// Forward BN: combine per-clip (mean, M2) partials (Chan et al.) into batch
-// mean / rstd for every channel; all threads end with them in stat[0..63].
-__device__ void bn_fwd_finalize(const float2* __restrict__ part, int B, float eps, float* red,
-                                float* stat, float* gstat, int tid) {
-  const int c = tid & 31, g = tid >> 5;   // 8 groups
-  float s = 0.f;
-  for (int b = g; b < B; b += 8) s += part[b * 32 + c].x;
-  red[g * 32 + c] = s;
-  __syncthreads();
-  float mean = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) mean += red[k * 32 + c];
-  mean /= (float)B;
-  float m2 = 0.f;
-  for (int b = g; b < B; b += 8) {
-    const float2 pb = part[b * 32 + c];
-    const float d = pb.x - mean;
-    m2 += pb.y + (float)NPIX * d * d;
-  }
-  __syncthreads();
-  red[g * 32 + c] = m2;
-  __syncthreads();
+// Forward BN: batch mean / rstd per channel from the fp64 sums of per-clip
+// (mean_b, mean_b^2, M2_b) (Chan et al.: M2 = sum M2_b + n (sum mean_b^2 -
+// (sum mean_b)^2 / B)); all threads end with them in stat[0..63].
+__device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps, float* stat,
+                                float* gstat, int tid) {
   if (tid < 32) {
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v += red[k * 32 + c];
-    v /= (float)B * (float)NPIX;
-    const float rstd = 1.0f / sqrtf(v + eps);
-    stat[c] = mean;
-    stat[32 + c] = rstd;
-    if (gstat) { gstat[c] = mean; gstat[32 + c] = rstd; }
+    const double s1 = acc[tid], s2 = acc[32 + tid], s3 = acc[64 + tid];
+    const double mean = s1 / B;
+    double m2 = s3 + (double)NPIX * (s2 - s1 * s1 / B);
+    m2 = m2 > 0.0 ? m2 : 0.0;
+    const float var = (float)(m2 / ((double)B * NPIX));
+    const float rstd = 1.0f / sqrtf(var + eps);
+    stat[tid] = (float)mean;
+    stat[32 + tid] = rstd;
+    if (gstat) { gstat[tid] = (float)mean; gstat[32 + tid] = rstd; }
   }
   __syncthreads();
 }
 
-// Backward BN: sum per-clip (sum dy, sum dy*xhat) -> means, in stat[0..63].
-__device__ void bn_bwd_finalize(const float2* __restrict__ part, int B, float* red, float* stat,
-                                int tid) {
-  const int c = tid & 31, g = tid >> 5;
-  float s0 = 0.f, s1 = 0.f;
-  for (int b = g; b < B; b += 8) { const float2 v = part[b * 32 + c]; s0 += v.x; s1 += v.y; }
-  red[g * 32 + c] = s0;
-  red[256 + g * 32 + c] = s1;
-  __syncthreads();
+// Backward BN: means of dy and dy*xhat from the fp64 sums, in stat[0..63].
+__device__ void bn_bwd_finalize(const double* __restrict__ acc, int B, float* stat, int tid) {
   if (tid < 32) {
-    float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { a0 += red[k * 32 + c]; a1 += red[256 + k * 32 + c]; }
-    const float inv = 1.f / ((float)B * (float)NPIX);
-    stat[c] = a0 * inv;
-    stat[32 + c] = a1 * inv;
+    const double inv = 1.0 / ((double)B * NPIX);
+    stat[tid] = (float)(acc[tid] * inv);
+    stat[32 + tid] = (float)(acc[32 + tid] * inv);
   }
   __syncthreads();
 }
 
 // Per-clip (mean, M2) of the conv outputs held in acc (two-pass, robust).
-__device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, float2* out, int lane,
+__device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out, int lane,
                                int wave, int tid) {
   float s = 0.f;
 #pragma unroll
@@ -195,7 +171,9 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, float2* out
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) v += red[w * 32 + tid];
-    out[tid] = make_float2(mean, v);
+    unsafeAtomicAdd(out + tid, (double)mean);
+    unsafeAtomicAdd(out + 32 + tid, (double)mean * (double)mean);
+    unsafeAtomicAdd(out + 64 + tid, (double)v);
   }
 }
 
@@ -237,7 +215,7 @@ __device__ void flush_gate(const f32x16& acc, float* scr, float* dst, int lane, 
 }
 
 // Workgroup totals of two per-lane channel sums -> out[b][c] (BN bwd partials)
-__device__ void bn_bwd_partial(float s0, float s1, float* red, float2* out, int lane, int wave,
+__device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int lane, int wave,
                                int tid) {
   s0 += __shfl_xor(s0, 32);
   s1 += __shfl_xor(s1, 32);
@@ -247,7 +225,8 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, float2* out, int 
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) { a += red[w * 32 + tid]; b += red[128 + w * 32 + tid]; }
-    out[tid] = make_float2(a, b);
+    unsafeAtomicAdd(out + tid, (double)a);
+    unsafeAtomicAdd(out + 32 + tid, (double)b);
   }
   __syncthreads();
 }
@@ -274,7 +253,7 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_a(CellArgs<S> a) {
 
   if (t < T) stage_x(a.x, L.xs, b, t, T, tid);
   if (t > 0)
-    bn_fwd_finalize(a.part1, B, a.eps, L.red, L.stat + 64,
+    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * 96, B, a.eps, L.stat + 64,
                     b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
   if (t < T && !a.no_inh) tile_zero<S>(tile, tid);
   __syncthreads();
@@ -341,7 +320,7 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_a(CellArgs<S> a) {
 #pragma unroll
   for (int i = 0; i < RPW; ++i)
     store_cl(a.ci + t * fs + cb + (size_t)(wave * RPW + i) * IMG * C, c, h, acc[i]);
-  bn_fwd_partial(acc, L.red, a.part0 + b * 32, lane, wave, tid);
+  bn_fwd_partial(acc, L.red, a.bnacc + ((size_t)t * 2 + 0) * 96, lane, wave, tid);
 }
 
 // =========================================================================
@@ -363,7 +342,7 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_b(CellArgs<S> a) {
 
   if (!a.no_inh) {
     stage_x(a.x, L.xs, b, t, T, tid);
-    bn_fwd_finalize(a.part0, B, a.eps, L.red, L.stat,
+    bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * 96, B, a.eps, L.stat,
                     b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   }
   tile_zero<S>(tile, tid);
@@ -412,7 +391,7 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_b(CellArgs<S> a) {
 #pragma unroll
   for (int i = 0; i < RPW; ++i)
     store_cl(a.ce + t * fs + cb + (size_t)(wave * RPW + i) * IMG * C, c, h, acc[i]);
-  bn_fwd_partial(acc, L.red, a.part1 + b * 32, lane, wave, tid);
+  bn_fwd_partial(acc, L.red, a.bnacc + ((size_t)t * 2 + 1) * 96, lane, wave, tid);
 }
 
 // =========================================================================
@@ -443,7 +422,7 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_a(CellArgs<S> a) {
 
   if (tail) {
     stage_x(a.x, L.xs, b, tt, T, tid);
-    if (!a.no_inh) bn_bwd_finalize(a.bpart0, B, L.red, L.stat, tid);
+    if (!a.no_inh) bn_bwd_finalize(a.bnbacc + ((size_t)tt * 2 + 0) * 64, B, L.stat, tid);
   }
   if (conv) tile_zero<S>(tile, tid);
   __syncthreads();
@@ -562,7 +541,7 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_a(CellArgs<S> a) {
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
-  if (head) bn_bwd_partial(bs0, bs1, L.red, a.bpart1 + b * 32, lane, wave, tid);
+  if (head) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * 64, lane, wave, tid);
   flush_small<9>(sm, slots, L.small, slab_b, lane, wave, tid);
   if (tail && head) {
     flush_gate(gaw, L.scr, slab_b + 0 * 1024, lane, wave, tid);
@@ -591,7 +570,7 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_b(CellArgs<S> a) {
   float* slab_b = a.slab + (size_t)b * SLAB;
 
   stage_x(a.x, L.xs, b, t, T, tid);
-  bn_bwd_finalize(a.bpart1, B, L.red, L.stat, tid);
+  bn_bwd_finalize(a.bnbacc + ((size_t)t * 2 + 1) * 64, B, L.stat, tid);
   tile_zero<S>(tile, tid);
   __syncthreads();
 
@@ -708,7 +687,7 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_b(CellArgs<S> a) {
   }
   sm[4] = bs1;
   sm[5] = bs0;
-  if (!a.no_inh) bn_bwd_partial(bs0, bs1, L.red, a.bpart0 + b * 32, lane, wave, tid);
+  if (!a.no_inh) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * 64, lane, wave, tid);
   flush_small<7>(sm, slots, L.small, slab_b, lane, wave, tid);
   if (!a.no_inh) {
     flush_gate(giw, L.scr, slab_b + 2 * 1024, lane, wave, tid);
@@ -998,6 +977,42 @@ static int fail(int code, const char* fmt, const char* a = "", long v = 0) {
 
 namespace {
 
+// ---- optional per-kind kernel timing (process-wide, mutex-guarded; autograd
+// launches the backward from its own device thread, so this cannot be
+// thread-local; see pt_cell.h) ----
+struct Timing {
+  std::mutex mu;
+  uint32_t mask = 0;
+  std::vector<hipEvent_t> pool;        // reusable events
+  size_t used = 0;
+  std::vector<int> kind;               // per recorded pair
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+};
+Timing g_tm;
+
+hipEvent_t tm_event() {
+  if (g_tm.used == g_tm.pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    g_tm.pool.push_back(e);
+  }
+  return g_tm.pool[g_tm.used++];
+}
+
+// Launch wrapper: brackets the launch with events when its kind is enabled.
+template <typename F>
+void timed(int kind, hipStream_t st, F&& launch) {
+  if (!(__atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) & (1u << kind))) { launch(); return; }
+  std::lock_guard<std::mutex> lk(g_tm.mu);
+  hipEvent_t a = tm_event(), b = tm_event();
+  if (!a || !b) { launch(); return; }
+  (void)hipEventRecord(a, st);
+  launch();
+  (void)hipEventRecord(b, st);
+  g_tm.kind.push_back(kind);
+  g_tm.ev.emplace_back(a, b);
+}
+
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
@@ -1008,7 +1023,7 @@ struct Plan {
   // saved offsets
   size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_bnstat, o_wf[4], o_g[12], saved;
   // workspace offsets
-  size_t o_part0, o_part1, o_bpart0, o_bpart1, o_tr[9], o_dci, o_dce, o_slab, o_wslab, ws;
+  size_t o_bnacc, o_bnbacc, o_tr[9], o_dci, o_dce, o_slab, o_wslab, ws;
   int nwg;
 };
 
@@ -1044,11 +1059,8 @@ Plan plan(const pt_cell_desc* d) {
   for (int i = 0; i < 12; ++i) { p.o_g[i] = o; o += al((size_t)C * C * p.es); }
   p.saved = o;
   o = 0;
-  const size_t part = al((size_t)p.B * 32 * 8);
-  p.o_part0 = o; o += part;
-  p.o_part1 = o; o += part;
-  p.o_bpart0 = o; o += part;
-  p.o_bpart1 = o; o += part;
+  p.o_bnacc = o; o += al((size_t)p.T * 2 * 96 * 8);
+  p.o_bnbacc = o; o += al((size_t)p.T * 2 * 64 * 8);
   for (int i = 0; i < 9; ++i) { p.o_tr[i] = o; o += al(p.frame * 4); }
   p.o_dci = o; o += fbytes;
   p.o_dce = o; o += fbytes;
@@ -1080,8 +1092,8 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
   a.ci = (S*)(saved + p.o_ci); a.ce = (S*)(saved + p.o_ce); a.eg = (S*)(saved + p.o_eg);
   a.bnstat = (float*)(saved + p.o_bnstat);
   if (ws) {
-    a.part0 = (float2*)(ws + p.o_part0); a.part1 = (float2*)(ws + p.o_part1);
-    a.bpart0 = (float2*)(ws + p.o_bpart0); a.bpart1 = (float2*)(ws + p.o_bpart1);
+    a.bnacc = (double*)(ws + p.o_bnacc);
+    a.bnbacc = (double*)(ws + p.o_bnbacc);
     float** tr[9] = {&a.dEn, &a.dcE, &a.dIl, &a.dEp, &a.dcI, &a.GI, &a.dgEp, &a.dxp, nullptr};
     for (int i = 0; i < 8; ++i) *tr[i] = (float*)(ws + p.o_tr[i]);
     a.GEfin = (const float*)(ws + p.o_tr[8]);
@@ -1126,12 +1138,13 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   }
   pa.wf_inh = (S*)((char*)saved + p.o_wf[0]); pa.wf_exc = (S*)((char*)saved + p.o_wf[1]);
   pa.wt_inh = (S*)((char*)saved + p.o_wf[2]); pa.wt_exc = (S*)((char*)saved + p.o_wf[3]);
-  hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa);
+  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnacc, 0, (size_t)p.T * 2 * 96 * 8, st));
+  timed(PT_K_PREP, st, [&] { hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa); });
   const size_t lds = cell_lds_bytes<S>();
   for (int t = 0; t <= p.T; ++t) {
     a.t = t;
-    hipLaunchKernelGGL(k_fwd_a<S>, dim3(p.B), dim3(NT), lds, st, a);
-    if (t < p.T) hipLaunchKernelGGL(k_fwd_b<S>, dim3(p.B), dim3(NT), lds, st, a);
+    timed(PT_K_FWD_A, st, [&] { hipLaunchKernelGGL(k_fwd_a<S>, dim3(p.B), dim3(NT), lds, st, a); });
+    if (t < p.T) timed(PT_K_FWD_B, st, [&] { hipLaunchKernelGGL(k_fwd_b<S>, dim3(p.B), dim3(NT), lds, st, a); });
   }
   if (e_last)
     hipLaunchKernelGGL(k_to_nchw<S>, dim3(256), dim3(256), 0, st,
@@ -1149,20 +1162,21 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
   HIPCHK(hipMemsetAsync((char*)ws + p.o_slab, 0, (size_t)p.B * SLAB * 4, st));
+  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnbacc, 0, (size_t)p.T * 2 * 64 * 8, st));
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[8]), p.B);
   const size_t lds = cell_lds_bytes<S>();
   a.t = p.T - 1;
-  hipLaunchKernelGGL(k_bwd_a<S>, dim3(p.B), dim3(NT), lds, st, a);
+  timed(PT_K_BWD_A, st, [&] { hipLaunchKernelGGL(k_bwd_a<S>, dim3(p.B), dim3(NT), lds, st, a); });
   for (int t = p.T - 1; t >= 0; --t) {
     a.t = t;
-    hipLaunchKernelGGL(k_bwd_b<S>, dim3(p.B), dim3(NT), lds, st, a);
+    timed(PT_K_BWD_B, st, [&] { hipLaunchKernelGGL(k_bwd_b<S>, dim3(p.B), dim3(NT), lds, st, a); });
     a.t = t - 1;
-    hipLaunchKernelGGL(k_bwd_a<S>, dim3(p.B), dim3(NT), lds, st, a);
+    timed(PT_K_BWD_A, st, [&] { hipLaunchKernelGGL(k_bwd_a<S>, dim3(p.B), dim3(NT), lds, st, a); });
   }
   float* wslab = (float*)((char*)ws + p.o_wslab);
   if (!d->no_inh) {
-    hipLaunchKernelGGL(k_wgrad<S>, dim3(p.nwg, 2), dim3(NT), wgrad_lds_bytes<S>(), st, a, wslab, p.nwg);
+    timed(PT_K_WGRAD, st, [&] { hipLaunchKernelGGL(k_wgrad<S>, dim3(p.nwg, 2), dim3(NT), wgrad_lds_bytes<S>(), st, a, wslab, p.nwg); });
   } else {
     HIPCHK(hipMemsetAsync(wslab, 0, (size_t)p.nwg * MAXTAP * 1024 * 4, st));
     // conv 1 only (w_exc); conv 0 slab stays zero
@@ -1177,7 +1191,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   if (d->no_inh) { r.g.w_inh = nullptr; r.g.alpha = nullptr; r.g.mu = nullptr;
                    r.g.bn_w[0] = nullptr; r.g.bn_b[0] = nullptr;
                    r.g.gate_w[2] = r.g.gate_w[3] = nullptr; r.g.gate_b[2] = r.g.gate_b[3] = nullptr; }
-  hipLaunchKernelGGL(k_reduce, dim3(256), dim3(256), 0, st, r);
+  timed(PT_K_REDUCE, st, [&] { hipLaunchKernelGGL(k_reduce, dim3(256), dim3(256), 0, st, r); });
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1228,6 +1242,38 @@ int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params
   if (d->dtype == PT_DTYPE_BF16)
     return run_backward<bf16_t>(d, x, p, saved, ws, d_e_last, g, (hipStream_t)stream);
   return run_backward<float>(d, x, p, saved, ws, d_e_last, g, (hipStream_t)stream);
+}
+
+int pt_cell_timing_enable(uint32_t kind_mask) {
+  __atomic_store_n(&g_tm.mask, kind_mask, __ATOMIC_RELAXED);
+  return 0;
+}
+
+int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches) {
+  if (!total_ms || !launches) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
+  std::lock_guard<std::mutex> lk(g_tm.mu);
+  double tot = 0.0;
+  int64_t n = 0;
+  for (size_t i = 0; i < g_tm.ev.size(); ++i) {
+    if (g_tm.kind[i] != kind) continue;
+    HIPCHK(hipEventSynchronize(g_tm.ev[i].second));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, g_tm.ev[i].first, g_tm.ev[i].second));
+    tot += ms;
+    ++n;
+  }
+  *total_ms = tot;
+  *launches = n;
+  return 0;
+}
+
+int pt_cell_timing_reset(void) {
+  std::lock_guard<std::mutex> lk(g_tm.mu);
+  for (auto& e : g_tm.ev) { (void)hipEventSynchronize(e.second); }
+  g_tm.ev.clear();
+  g_tm.kind.clear();
+  g_tm.used = 0;
+  return 0;
 }
 
 const char* pt_last_error(void) { return g_err; }

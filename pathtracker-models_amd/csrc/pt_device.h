@@ -113,17 +113,25 @@ __device__ __forceinline__ float hsum16(const f32x16& v) {
 }
 
 // ---------------------------------------------------------------- activations
-// nl = softplus(beta=1, threshold=20) or tanh (models/InT.py:184, engine.py:145)
+// nl = softplus(beta=1, threshold=20) or tanh (models/InT.py:184, engine.py:145).
+// Hardware exp/log/rcp (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp): absolute
+// deviations from libm are O(1e-7), far inside the 1e-3 parity bound.
+__device__ __forceinline__ float fexp(float x) { return __expf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float sigm(float x) { return frcp(1.f + fexp(-x)); }
+__device__ __forceinline__ float ftanh(float x) {
+  const float t = 1.f - 2.f * frcp(fexp(2.f * fabsf(x)) + 1.f);
+  return copysignf(t, x);
+}
 __device__ __forceinline__ float act_f(float x, int act) {
-  if (act == 0) return x > 20.f ? x : log1pf(expf(x));
-  return tanhf(x);
+  if (act == 0) return x > 20.f ? x : __logf(1.f + fexp(x));
+  return ftanh(x);
 }
 __device__ __forceinline__ float act_d(float x, int act) {   // d nl / d x
-  if (act == 0) return x > 20.f ? 1.f : 1.f / (1.f + expf(-x));
-  const float t = tanhf(x);
+  if (act == 0) return x > 20.f ? 1.f : sigm(x);
+  const float t = ftanh(x);
   return 1.f - t * t;
 }
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 // --------------------------------------------------------- per-wave transpose
 // 32x32 f32 scratch, swizzled so the CL write and the PA read are both
@@ -234,42 +242,66 @@ __device__ void tile_fill(S* __restrict__ tile, const S* __restrict__ src, int p
 
 // Implicit-GEMM k x k conv over the LDS tile for this wave's RPW rows:
 //   acc[i][x][n] += sum_{tap,ci} in[row0+i+kh-pad][x+kw-pad][ci] * W[n][ci][tap]
-// wf: B fragments [K*K][KS][64] (prepared by k_prep).  The caller has zeroed
-// the tile halo; this routine refills the interior per pass.
-template <class S>
-__device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], const S* __restrict__ src,
-                         const typename Tr<S>::frag* __restrict__ wf, S* tile, int K, int row0,
-                         int tid, int lane) {
+// wf: B fragments [K*K][KS][64] (prepared by k_prep), streamed from L2 with a
+// two-tap-deep register prefetch so each tap's 16 (bf16) MFMAs never wait on
+// a global load.  The caller has zeroed the tile halo; the interior is refilled
+// per pass.
+template <class S, int K>
+__device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], const S* __restrict__ src,
+                                           const typename Tr<S>::frag* __restrict__ wf, S* tile,
+                                           int row0, int tid, int lane) {
   using TT = Tr<S>;
+  using F = typename TT::frag;
   constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
-  const int off = PADMAX - K / 2;
+  constexpr int KK = K * K;
+  constexpr int off = PADMAX - K / 2;
   const int h = lane >> 5, px = lane & 31;
   for (int pass = 0; pass < TT::NPASS; ++pass) {
     __syncthreads();
     tile_fill<S>(tile, src, pass, tid);
     __syncthreads();
-    for (int kh = 0; kh < K; ++kh) {
-      for (int kw = 0; kw < K; ++kw) {
-        const int tap = kh * K + kw;
-        const int tcol = px + kw + off;
+    const F* w = wf + pass * KSP * 64 + lane;
+    F b0[KSP], b1[KSP], b2[KSP];
 #pragma unroll
-        for (int s = 0; s < KSP; ++s) {
-          const int ks = pass * KSP + s;
-          const typename TT::frag b = wf[(tap * TT::KS + ks) * 64 + lane];
+    for (int s = 0; s < KSP; ++s) {
+      b0[s] = w[(0 * TT::KS + s) * 64];
+      b1[s] = w[((KK > 1 ? 1 : 0) * TT::KS + s) * 64];
+    }
+    for (int tap = 0; tap < KK; ++tap) {
+      const int tn = tap + 2 < KK ? tap + 2 : KK - 1;
 #pragma unroll
-          for (int i = 0; i < RPW; ++i) {
-            const int trow = row0 + i + kh + off;
-            typename TT::frag a;
-            if constexpr (sizeof(S) == 4) {
-              a = tile[tile_off<S>(trow, tcol, 2 * s + h)];
-            } else {
-              a = *(const bf16x8*)(tile + tile_off<S>(trow, tcol, 16 * s + 8 * h));
-            }
-            acc[i] = TT::mma(a, b, acc[i]);
+      for (int s = 0; s < KSP; ++s) b2[s] = w[(tn * TT::KS + s) * 64];
+      const int kh = tap / K, kw = tap - kh * K;
+      const int tcol = px + kw + off;
+#pragma unroll
+      for (int s = 0; s < KSP; ++s) {
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+          const int trow = row0 + i + kh + off;
+          F a;
+          if constexpr (sizeof(S) == 4) {
+            a = tile[tile_off<S>(trow, tcol, 2 * s + h)];
+          } else {
+            a = *(const bf16x8*)(tile + tile_off<S>(trow, tcol, 16 * s + 8 * h));
           }
+          acc[i] = TT::mma(a, b0[s], acc[i]);
         }
       }
+#pragma unroll
+      for (int s = 0; s < KSP; ++s) { b0[s] = b1[s]; b1[s] = b2[s]; }
     }
+  }
+}
+
+template <class S>
+__device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], const S* __restrict__ src,
+                                         const typename Tr<S>::frag* __restrict__ wf, S* tile,
+                                         int K, int row0, int tid, int lane) {
+  switch (K) {
+    case 7: conv_run_k<S, 7>(acc, src, wf, tile, row0, tid, lane); break;
+    case 5: conv_run_k<S, 5>(acc, src, wf, tile, row0, tid, lane); break;
+    case 3: conv_run_k<S, 3>(acc, src, wf, tile, row0, tid, lane); break;
+    default: conv_run_k<S, 1>(acc, src, wf, tile, row0, tid, lane); break;
   }
 }
 

@@ -19,7 +19,12 @@ PT_DTYPE_F32, PT_DTYPE_BF16 = 0, 1
 
 # Exported symbols declared in include/pt_cell.h (tests check all are present).
 EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
-           "pt_cell_export_exc", "pt_cell_backward", "pt_last_error", "pt_version")
+           "pt_cell_export_exc", "pt_cell_backward", "pt_cell_timing_enable",
+           "pt_cell_timing_read", "pt_cell_timing_reset", "pt_last_error", "pt_version")
+
+# kernel kinds for pt_cell_timing_* (include/pt_cell.h)
+K_FWD_A, K_FWD_B, K_BWD_A, K_BWD_B, K_WGRAD, K_PREP, K_REDUCE = range(7)
+KIND_NAMES = ("k_fwd_a", "k_fwd_b", "k_bwd_a", "k_bwd_b", "k_wgrad", "k_prep", "k_reduce")
 
 _P = ctypes.c_void_p
 
@@ -74,6 +79,12 @@ def load():
         lib.pt_cell_backward.restype = ctypes.c_int
         lib.pt_cell_backward.argtypes = [ctypes.POINTER(Desc), _P, ctypes.POINTER(Params), _P, _P,
                                          _P, ctypes.POINTER(Grads), _P]
+        lib.pt_cell_timing_enable.restype = ctypes.c_int
+        lib.pt_cell_timing_enable.argtypes = [ctypes.c_uint32]
+        lib.pt_cell_timing_read.restype = ctypes.c_int
+        lib.pt_cell_timing_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_int64)]
+        lib.pt_cell_timing_reset.restype = ctypes.c_int
         lib.pt_last_error.restype = ctypes.c_char_p
         lib.pt_version.restype = ctypes.c_char_p
         _lib = lib
@@ -84,3 +95,12 @@ def check(rc: int):
     if rc != 0:
         msg = load().pt_last_error().decode(errors="replace")
         raise PtCellError(f"pt_cell error {rc}: {msg}")
+
+
+def timing_read(kind: int):
+    """(total_ms, launches) of kernel kind since the last reset (synchronises)."""
+    lib = load()
+    ms = ctypes.c_double()
+    n = ctypes.c_int64()
+    check(lib.pt_cell_timing_read(kind, ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value
