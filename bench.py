@@ -57,15 +57,18 @@ def algorithmic_flops(kind, batch, frames):
 
     Counts the model's contractions only (no recompute): forward conv + gates;
     backward data-gradients + 1x1 weight-gradients; the k x k weight gradients
-    in k_wgrad.  Sum over kinds = 3 x forward = SURVEY.md §8(d)'s 41.9 GFLOP/clip
-    at T=64 (minus the stem's 12.6 MFLOP, counted nowhere)."""
+    in k_wgrad.  Sum over kinds = 3 x forward (41.9 GFLOP/clip
+    at T=64, minus the stem's 12.6 MFLOP which is counted nowhere)."""
     cf, gf = conv_flops(), gate_flops()
     per_clip = {
-        "k_fwd_a": frames * (cf + 4 * gf),          # conv(gE,w_inh) + a_w,a_u,e_w,e_u
-        "k_fwd_b": frames * (cf + 2 * gf),          # conv(I,w_exc) + i_w,i_u
-        "k_bwd_a": (frames - 1) * (cf + 4 * gf)     # conv^T(w_inh) + a_* dgrad/wgrad
-                   + frames * 0,
-        "k_bwd_b": frames * (cf + 8 * gf),          # conv^T(w_exc) + i_*,e_* dgrad/wgrad
+        "k_conv_fa": frames * cf,                   # conv(gE, w_inh)
+        "k_conv_fb": frames * cf,                   # conv(I, w_exc)
+        "k_pw_fa": frames * 4 * gf,                 # a_w, a_u, e_w, e_u
+        "k_pw_fb": frames * 2 * gf,                 # i_w, i_u
+        "k_conv_bb": frames * cf,                   # conv^T(w_exc)
+        "k_conv_ba": (frames - 1) * cf,             # conv^T(w_inh) (frame 0's is dead)
+        "k_pw_ba": (frames - 1) * 4 * gf,           # a_* dgrad + wgrad
+        "k_pw_bb": frames * 8 * gf,                 # i_*, e_* dgrad + wgrad
         "k_wgrad": frames * 2 * cf,                 # dW_inh + dW_exc
     }.get(kind, 0)
     return per_clip * batch
@@ -159,7 +162,7 @@ def main():
     torch.cuda.synchronize()
     lib = _lib.load()
     lib.pt_cell_timing_reset()
-    lib.pt_cell_timing_enable((1 << 7) - 1)
+    lib.pt_cell_timing_enable((1 << _lib.NKINDS) - 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -114,8 +114,9 @@ int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params
  * stream.  Reading
  * synchronises on the recorded events and returns the summed device time and
  * the launch count since the last reset.  Kinds: */
-enum { PT_K_FWD_A = 0, PT_K_FWD_B = 1, PT_K_BWD_A = 2, PT_K_BWD_B = 3, PT_K_WGRAD = 4,
-       PT_K_PREP = 5, PT_K_REDUCE = 6, PT_K_NKINDS = 7 };
+enum { PT_K_PW_FA = 0, PT_K_CONV_FA = 1, PT_K_PW_FB = 2, PT_K_CONV_FB = 3,
+       PT_K_PW_BA = 4, PT_K_CONV_BA = 5, PT_K_PW_BB = 6, PT_K_CONV_BB = 7,
+       PT_K_WGRAD = 8, PT_K_PREP = 9, PT_K_REDUCE = 10, PT_K_NKINDS = 11 };
 int pt_cell_timing_enable(uint32_t kind_mask);      /* bit k enables kind k; 0 disables */
 int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches);
 int pt_cell_timing_reset(void);

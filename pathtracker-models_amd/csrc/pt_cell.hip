@@ -19,6 +19,7 @@
 #include "../../include/pt_cell.h"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <mutex>
 #include <vector>
@@ -34,32 +35,7 @@ enum SmallSlot {
 };
 constexpr int SLAB_G = 6 * 1024;                 // 6 gate weights [n][ci]
 constexpr int SLAB = SLAB_G + NSMALL * 32;
-
-constexpr int MISC_FLOATS = 2560;
-template <class S>
-constexpr int cell_lds_bytes() {
-  return tile_bytes<S>() + NPIX * 16 /*xs*/ + NWAVE * 1024 * 4 /*scr*/ + MISC_FLOATS * 4;
-}
-
-struct Lds {
-  char* tile;
-  f32x4* xs;
-  float* scr;     // [NWAVE][1024]
-  float* stat;    // [4][32]
-  float* red;     // [512]
-  float* small;   // [NWAVE][NSMALL][32]
-};
-template <class S>
-__device__ __forceinline__ Lds carve(char* smem) {
-  Lds l;
-  l.tile = smem;
-  l.xs = (f32x4*)(smem + tile_bytes<S>());
-  l.scr = (float*)(smem + tile_bytes<S>() + NPIX * 16);
-  l.stat = l.scr + NWAVE * 1024;
-  l.red = l.stat + 128;
-  l.small = l.red + 512;
-  return l;
-}
+constexpr int NTRANS = 11;                       // backward transients incl. GEfin
 
 // ----------------------------------------------------------------- arguments
 template <class S>
@@ -68,6 +44,9 @@ struct CellArgs {
   int B, T, K, act, no_inh;
   float eps;
   int t;
+  int ablate;     // timing experiments only (env PT_CELL_ABLATE): 1 skip conv MFMAs,
+                  // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
+                  // atomics, 16 skip LDS weight-grad atomics, 32 skip slab flush
   const float* x;                       // [B][3][T][32][32]
   const float *wpre, *bpre;             // [32][3], [32]
   const float *alpha, *mu, *gamma, *kappa;
@@ -80,23 +59,25 @@ struct CellArgs {
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
   double* bnacc;                        // fwd BN sums [T][2][3][32]: sum mean_b, sum mean_b^2, sum M2_b
   float* gates;                         // [B][T][C][32][32] or null
-  // backward
-  float *dEn, *dcE, *dIl, *dEp, *dcI, *GI, *dgEp, *dxp;   // f32 [B][32][32][32]
-  const float* GEfin;                   // f32 channels-last dE of the last frame
+  // backward transients, channels-last [B][32][32][32] in the storage type
+  S *dEn, *dcE, *dIl, *dEp, *dcI, *GI, *dgEp, *dxp, *dgE, *dIt;
+  const float* GEfin;                   // dE of the last frame (channels-last)
   S *dci_s, *dce_s;                     // [T][B][32][32][32] conv-output grads (for k_wgrad)
   double* bnbacc;                       // bwd BN sums [T][2][2][32]: sum dy, sum dy*xhat
-  float* slab;                          // [B][SLAB]
+  float* slab;                          // [B][PW_PARTS][SLAB]
+  int conv_done;                        // k_pw_ba: dgE holds conv^T(w_inh) + dgEp
 };
 
 __device__ __forceinline__ size_t fr_off(int t, int B) { return (size_t)t * B * NPIX * C; }
 __device__ __forceinline__ size_t clip_off(int b) { return (size_t)b * NPIX * C; }
 
-// Stage x[b, 0:3, t] as float4 per pixel.
-__device__ void stage_x(const float* __restrict__ x, f32x4* xs, int b, int t, int T, int tid) {
-  const float* x0 = x + ((size_t)(b * 3 + 0) * T + t) * NPIX;
-  const float* x1 = x + ((size_t)(b * 3 + 1) * T + t) * NPIX;
-  const float* x2 = x + ((size_t)(b * 3 + 2) * T + t) * NPIX;
-  for (int p = tid; p < NPIX; p += NT) {
+// Stage rows [y0, y0+nrows) of x[b, 0:3, t] as float4 per pixel.
+__device__ void stage_x(const float* __restrict__ x, f32x4* xs, int b, int t, int T, int y0,
+                        int nrows, int tid, int nthreads) {
+  const float* x0 = x + ((size_t)(b * 3 + 0) * T + t) * NPIX + y0 * IMG;
+  const float* x1 = x + ((size_t)(b * 3 + 1) * T + t) * NPIX + y0 * IMG;
+  const float* x2 = x + ((size_t)(b * 3 + 2) * T + t) * NPIX + y0 * IMG;
+  for (int p = tid; p < nrows * IMG; p += nthreads) {
     f32x4 v;
     v[0] = x0[p]; v[1] = x1[p]; v[2] = x2[p]; v[3] = 0.f;
     xs[p] = v;
@@ -105,11 +86,11 @@ __device__ void stage_x(const float* __restrict__ x, f32x4* xs, int b, int t, in
 
 // Stem (models/InT.py:212-213): z = W_pre x + b; xbn = nl(z); CL layout.
 struct Stem { float w0, w1, w2, b; };
-__device__ __forceinline__ void stem_cl(const f32x4* xs, int y, int h, const Stem& st, int act,
+__device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const Stem& st, int act,
                                         f32x16& z, f32x16& xv) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const f32x4 v = xs[y * IMG + cl_x(r, h)];
+    const f32x4 v = xs[yl * IMG + cl_x(r, h)];
     z[r] = st.w0 * v[0] + st.w1 * v[1] + st.w2 * v[2] + st.b;
     xv[r] = act_f(z[r], act);
   }
@@ -134,17 +115,8 @@ __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps
   __syncthreads();
 }
 
-// Backward BN: means of dy and dy*xhat from the fp64 sums, in stat[0..63].
-__device__ void bn_bwd_finalize(const double* __restrict__ acc, int B, float* stat, int tid) {
-  if (tid < 32) {
-    const double inv = 1.0 / ((double)B * NPIX);
-    stat[tid] = (float)(acc[tid] * inv);
-    stat[32 + tid] = (float)(acc[32 + tid] * inv);
-  }
-  __syncthreads();
-}
-
-// Per-clip (mean, M2) of the conv outputs held in acc (two-pass, robust).
+// Per-clip (mean, M2) of the conv outputs held in acc (two-pass, robust),
+// accumulated into the fp64 batch sums.
 __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out, int lane,
                                int wave, int tid) {
   float s = 0.f;
@@ -177,10 +149,214 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out
   }
 }
 
-// Workgroup sum of per-lane values for the lane's channel (halves combined):
-// small[] gets every wave's contribution; thread tid<32*n reads totals.
+// =========================================================================
+// Conv kernels: one workgroup (4 waves x 8 rows) per clip; the whole 32x32
+// clip image is one zero-halo LDS tile.  FILL: how the tile interior is
+// produced; EPI: what happens to the conv result.
+//   FILL_COPY   input image as stored (forward: gE_t or I_t)
+//   FILL_BNBWD  BatchNorm backward applied on the fly (models/InT.py:161/:172
+//               reversed): dx = rstd g (dy - mean(dy) - xhat mean(dy xhat)),
+//               also written out (the k x k weight gradient's D operand)
+//   EPI_FWD     store the pre-BN conv output + per-clip BN statistics
+//   EPI_ADD     out = conv + add0 (+ add1), f32
+//   EPI_NONE    fill only (frame 0's dci: needed by k_wgrad, conv^T dead)
+// =========================================================================
+enum { FILL_COPY = 0, FILL_BNBWD = 1 };
+enum { EPI_FWD = 0, EPI_ADD = 1, EPI_NONE = 2 };
+
+template <class S>
+struct ConvArgs {
+  using F = typename Tr<S>::frag;
+  int B, K, ablate;
+  const S* src;                 // FILL_COPY: frame base [B][NPIX][C]
+  const S* dc;                  // FILL_BNBWD: dy
+  const S* raw;                 // FILL_BNBWD: pre-BN conv output of the forward
+  const float* bnstat;          // FILL_BNBWD: mean[32], rstd[32]
+  const double* bnb;            // FILL_BNBWD: sum dy[32], sum dy*xhat[32]
+  const float* bnw;             // FILL_BNBWD: BN gamma
+  S* fill_out;                  // FILL_BNBWD: dx written here too
+  const F* wf;
+  S* out_raw;                   // EPI_FWD
+  double* bnacc;                // EPI_FWD
+  S* out;                       // EPI_ADD
+  const S *add0, *add1;         // EPI_ADD (add1 may be null)
+};
+
+constexpr int CONV_MISC = 512;  // floats: red[128] + bn-bwd table [3][32]
+template <class S>
+constexpr int conv_lds_bytes() { return tile_bytes<S>() + CONV_MISC * 4; }
+
+template <class S, int FILL, int EPI>
+__global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  S* tile = (S*)smem;
+  float* red = (float*)(smem + tile_bytes<S>());
+  float* tbl = red + 128;       // FILL_BNBWD: per-channel A, Bc, Cc
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x;
+  const size_t cb = clip_off(b);
+
+  if constexpr (FILL == FILL_BNBWD) {
+    if (tid < 32) {
+      // dx = A dy + Bc raw + Cc  with A = rstd g, xhat = (raw - mean) rstd
+      const double inv = 1.0 / ((double)a.B * NPIX);
+      const float md = (float)(a.bnb[tid] * inv), mdx = (float)(a.bnb[32 + tid] * inv);
+      const float mean = a.bnstat[tid], rstd = a.bnstat[32 + tid];
+      const float A = rstd * a.bnw[tid];
+      tbl[tid] = A;
+      tbl[32 + tid] = -A * mdx * rstd;
+      tbl[64 + tid] = -A * md + A * mdx * rstd * mean;
+    }
+  }
+  if constexpr (EPI != EPI_NONE) tile_zero<S>(tile, tid);
+  __syncthreads();
+
+  auto fill = [&](int pass) {
+    if constexpr (FILL == FILL_COPY) {
+      tile_fill<S>(tile, a.src + cb, pass, tid);
+    } else {
+      constexpr int CPB = 16 / (int)sizeof(S);      // channels per 16-B chunk of S
+      constexpr int NCH = Tr<S>::CP / CPB;
+      constexpr int PER = NPIX * NCH / NT;           // 16 chunks per thread
+      constexpr int BATCH = 4;
+#pragma unroll
+      for (int k0 = 0; k0 < PER; k0 += BATCH) {
+        uint4 dv[BATCH], rv[BATCH];
+#pragma unroll
+        for (int k = 0; k < BATCH; ++k) {
+          const int idx = tid + (k0 + k) * NT;
+          const int pix = idx / NCH, q = idx % NCH;
+          const size_t e = cb + (size_t)pix * C + pass * Tr<S>::CP + q * CPB;
+          dv[k] = *(const uint4*)(a.dc + e);
+          rv[k] = *(const uint4*)(a.raw + e);
+        }
+#pragma unroll
+        for (int k = 0; k < BATCH; ++k) {
+          const int idx = tid + (k0 + k) * NT;
+          const int pix = idx / NCH, q = idx % NCH;
+          const int ch0 = pass * Tr<S>::CP + q * CPB;
+          const S* rr = (const S*)&rv[k];
+          const S* dd = (const S*)&dv[k];
+          uint4 ov;
+          S* oo = (S*)&ov;
+#pragma unroll
+          for (int j = 0; j < CPB; ++j) {
+            const int ch = ch0 + j;
+            const float v = tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch];
+            oo[j] = (S)v;
+          }
+          *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
+          if constexpr (EPI != EPI_NONE) {
+            const int y = pix >> 5, x = pix & 31;
+            *(uint4*)(tile + tile_off<S>(y + PADMAX, x + PADMAX, q * CPB)) = ov;
+          }
+        }
+      }
+    }
+  };
+
+  if constexpr (EPI == EPI_NONE) {
+    for (int pass = 0; pass < Tr<S>::NPASS; ++pass) fill(pass);
+    return;
+  } else {
+    f32x16 acc[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) acc[i] = zero16();
+    conv_run<S>(acc, fill, a.wf, tile, a.K, wave * RPW, lane, a.ablate);
+    if constexpr (EPI == EPI_FWD) {
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+        store_cl(a.out_raw + cb + (size_t)(wave * RPW + i) * IMG * C, c, h, acc[i]);
+      bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
+    } else {
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        const size_t ro = cb + (size_t)(wave * RPW + i) * IMG * C;
+        f32x16 v = acc[i] + load_cl(a.add0 + ro, c, h);
+        if (a.add1) v += load_cl(a.add1 + ro, c, h);
+        store_cl(a.out + ro, c, h, v);
+      }
+    }
+  }
+}
+
+// =========================================================================
+// Point-wise kernels: 8 waves per workgroup, each wave owns PW_RPP image rows
+// (1 in the forward, 2 in the backward), several workgroups per CU: the long
+// dependent element-wise / 1x1-gate chains are hidden by occupancy.
+// =========================================================================
+constexpr int PW_NT = 512;
+constexpr int PW_NW = PW_NT / 64;
+constexpr int PWF_RPP = 1;                         // forward rows per wave
+constexpr int PWB_RPP = 2;                         // backward rows per wave
+constexpr int PWF_WGPC = IMG / (PW_NW * PWF_RPP);  // workgroups per clip (4)
+constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (2)
+constexpr int PW_PARTS = PWB_WGPC;                 // slab partitions per clip
+
+constexpr int PW_NGACC = 4;   // 1x1 weight-gradient tiles accumulated in LDS per workgroup
+template <int RPP>
+constexpr int pw_lds_bytes() {   // forward point-wise kernels use xs, scr, stat only
+  return RPP == PWF_RPP
+             ? PW_NW * RPP * IMG * 16 + PW_NW * SCR_FLOATS * 4 + 128 * 4
+             : PW_NW * RPP * IMG * 16 /*xs*/ + PW_NW * SCR_FLOATS * 4 /*scr*/ + 128 * 4 /*stat*/ +
+                   PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ +
+                   PW_NGACC * 1024 * 4 /*gacc*/ + PW_NW * 1024 * 4 /*flush*/;
+}
+struct PLds {
+  f32x4* xs;
+  float* scr;     // [PW_NW][SCR_FLOATS]
+  float* stat;    // [128]
+  float* small;   // [PW_NW][NSMALL][32]
+  float* red;     // [512]
+  float* gacc;    // [PW_NGACC][1024]  (rows n, cols ci)
+  float* flush;   // [PW_NW][1024]     per-wave weight-gradient tiles of one gate
+};
+template <int RPP>
+__device__ __forceinline__ PLds pcarve(char* smem) {
+  PLds l;
+  l.xs = (f32x4*)smem;
+  l.scr = (float*)(smem + PW_NW * RPP * IMG * 16);
+  l.stat = l.scr + PW_NW * SCR_FLOATS;
+  l.small = l.stat + 128;
+  l.red = l.small + PW_NW * NSMALL * 32;
+  l.gacc = l.red + 512;
+  l.flush = l.gacc + PW_NGACC * 1024;
+  return l;
+}
+
+// Add one row's 1x1 weight-gradient tile (dW[n][ci] = sum_p D[p][n] X[p][ci],
+// one MFMA pair from CL registers) into the workgroup accumulator: every wave
+// parks its tile in its own flush slot, then each thread sums its elements
+// over the waves (plain stores, no atomics; all waves call this uniformly).
+template <class S>
+__device__ __forceinline__ void gacc_row(float* gacc_g, float* flush, const f32x16& d,
+                                         const f32x16& x, int lane, int wave, int tid) {
+  const f32x16 t = wgrad_cl<S>(d, x, zero16());
+  const int ci = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) flush[wave * 1024 + cl_x(r, h) * 32 + ci] = t[r];
+  __syncthreads();
+  for (int e = tid; e < 1024; e += PW_NT) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < PW_NW; ++w) s += flush[w * 1024 + e];
+    gacc_g[e] += s;
+  }
+  __syncthreads();
+}
+__device__ void gacc_zero(float* g, int n, int tid) {
+  for (int e = tid; e < n * 1024; e += PW_NT) g[e] = 0.f;
+}
+// slab[dst_gate[k]] += gacc[k] for k < n (after a barrier)
+__device__ void gacc_flush(const float* g, float* slab_p, int g0, int n, int tid) {
+  for (int e = tid; e < n * 1024; e += PW_NT) slab_p[(g0 + e / 1024) * 1024 + e % 1024] += g[e];
+}
+
+// Workgroup sum of per-lane channel values -> slab (RMW, this workgroup's
+// partition only: no atomics).
 template <int N>
-__device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, float* slab_b,
+__device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, float* slab_p,
                             int lane, int wave, int tid) {
 #pragma unroll
   for (int k = 0; k < N; ++k) {
@@ -188,83 +364,69 @@ __device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, f
     if (lane < 32) small[(wave * N + k) * 32 + lane] = s;
   }
   __syncthreads();
-  for (int e = tid; e < N * 32; e += NT) {
+  for (int e = tid; e < N * 32; e += PW_NT) {
     const int k = e >> 5, c = e & 31;
     float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) s += small[(w * N + k) * 32 + c];
-    slab_b[SLAB_G + slot[k] * 32 + c] += s;
+    for (int w = 0; w < PW_NW; ++w) s += small[(w * N + k) * 32 + c];
+    slab_p[SLAB_G + slot[k] * 32 + c] += s;
   }
   __syncthreads();
 }
 
-// Sum a per-wave 1x1 weight-gradient tile (rows n, cols ci) over the waves
-// and add it into the clip's slab.
-__device__ void flush_gate(const f32x16& acc, float* scr, float* dst, int lane, int wave, int tid) {
-  const int ci = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) scr[wave * 1024 + cl_x(r, h) * 32 + ci] = acc[r];
-  __syncthreads();
-  for (int e = tid; e < 1024; e += NT) {
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWAVE; ++w) s += scr[w * 1024 + e];
-    dst[e] += s;
-  }
-  __syncthreads();
-}
-
-// Workgroup totals of two per-lane channel sums -> out[b][c] (BN bwd partials)
+// Workgroup totals of two per-lane channel sums -> fp64 batch sums.
 __device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int lane, int wave,
                                int tid) {
   s0 += __shfl_xor(s0, 32);
   s1 += __shfl_xor(s1, 32);
-  if (lane < 32) { red[wave * 32 + lane] = s0; red[128 + wave * 32 + lane] = s1; }
+  if (lane < 32) { red[wave * 32 + lane] = s0; red[256 + wave * 32 + lane] = s1; }
   __syncthreads();
   if (tid < 32) {
     float a = 0.f, b = 0.f;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) { a += red[w * 32 + tid]; b += red[128 + w * 32 + tid]; }
+    for (int w = 0; w < PW_NW; ++w) { a += red[w * 32 + tid]; b += red[256 + w * 32 + tid]; }
     unsafeAtomicAdd(out + tid, (double)a);
     unsafeAtomicAdd(out + 32 + tid, (double)b);
   }
   __syncthreads();
 }
 
-// =========================================================================
-// Forward A (frame t, 0 <= t <= T):
+// -------------------------------------------------------------------------
+// Forward point-wise A (frame t, 0 <= t <= T):
 //   t > 0 : close frame t-1: E_{t-1} = (1-eg) E_{t-2} + eg nl(BN1(ce) (kappa I_{t-1} + gamma))
 //           (models/InT.py:172-175)
 //   t < T : att = sig(a_w x_t + a_u E_{t-1}) (:148), gE = att*E_{t-1} (:153),
-//           eg = sig(e_w I_{t-1} + e_u gE) (:171, uses the OLD inhibition),
-//           ci = conv(gE, w_inh) (:161) -> BN0 partials
-// =========================================================================
+//           eg = sig(e_w I_{t-1} + e_u gE) (:171, uses the OLD inhibition;
+//           no_inh: e_w E_{t-1}, :168)
+// -------------------------------------------------------------------------
 template <class S>
-__global__ __launch_bounds__(NT, 1) void k_fwd_a(CellArgs<S> a) {
+__global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds L = carve<S>(smem);
-  S* tile = (S*)L.tile;
+  const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, t = a.t, T = a.T, B = a.B;
-  float* wscr = L.scr + wave * 1024;
+  const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
+  const int t = a.t, T = a.T, B = a.B;
+  const int y0 = part * PW_NW * PWF_RPP;
+  float* wscr = L.scr + wave * SCR_FLOATS;
   const size_t fs = fr_off(1, B), cb = clip_off(b);
 
-  if (t < T) stage_x(a.x, L.xs, b, t, T, tid);
+  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW * PWF_RPP, tid, PW_NT);
   if (t > 0)
     bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * 96, B, a.eps, L.stat + 64,
-                    b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
-  if (t < T && !a.no_inh) tile_zero<S>(tile, tid);
+                    blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
   __syncthreads();
+  if (a.ablate & 4) return;
 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float kap = a.kappa[c], gam = a.gamma[c], bw1 = a.bnw1[c], bb1 = a.bnb1[c];
   const float m1 = L.stat[64 + c], rs1 = L.stat[96 + c];
   const float ba = a.gb[0][c] + a.gb[1][c], be = a.gb[4][c] + a.gb[5][c];
 
-  for (int i = 0; i < RPW; ++i) {
-    const int y = wave * RPW + i;
+#pragma unroll 1
+  for (int i = 0; i < PWF_RPP; ++i) {
+    const int yl = wave * PWF_RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 Ep = zero16(), Iv = zero16();
     if (t > 0) {
@@ -282,7 +444,7 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_a(CellArgs<S> a) {
     }
     if (t == T) continue;
     f32x16 z, xv;
-    stem_cl(L.xs, y, h, st, a.act, z, xv);
+    stem_cl(L.xs, yl, h, st, a.act, z, xv);
     F pax[Tr<S>::KS], pae[Tr<S>::KS];
     cl_to_pa<S>(wscr, xv, lane, pax);
     cl_to_pa<S>(wscr, Ep, lane, pae);
@@ -298,7 +460,6 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_a(CellArgs<S> a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) gp[cl_x(r, h)] = att[r];
     }
-    // exc gate input: gated inhibition = old I (InT) or E (no_inh, :168)
     const f32x16 ginh = a.no_inh ? Ep : Iv;
     F pag[Tr<S>::KS], pai[Tr<S>::KS];
     cl_to_pa<S>(wscr, gEv, lane, pag);
@@ -311,57 +472,49 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_a(CellArgs<S> a) {
     for (int r = 0; r < 16; ++r) egn[r] = sigm(acc[r] + be);
     store_cl(a.eg + t * fs + ro, c, h, egn);
   }
-  if (t == T || a.no_inh) return;
-
-  f32x16 acc[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) acc[i] = zero16();
-  conv_run<S>(acc, a.gE + t * fs + cb, a.wf_inh, tile, a.K, wave * RPW, tid, lane);
-#pragma unroll
-  for (int i = 0; i < RPW; ++i)
-    store_cl(a.ci + t * fs + cb + (size_t)(wave * RPW + i) * IMG * C, c, h, acc[i]);
-  bn_fwd_partial(acc, L.red, a.bnacc + ((size_t)t * 2 + 0) * 96, lane, wave, tid);
 }
 
-// =========================================================================
-// Forward B (frame t):  BN0 -> Ihat = nl(x - nl(c_i (alpha I + mu))) (:162),
-//   ig = sig(i_w x + i_u I) (:165), I_t = (1-ig) I + ig Ihat (:166)
-//   [no_inh: I_t = gE (:168)];  ce = conv(I_t, w_exc) (:172) -> BN1 partials
-// =========================================================================
+// -------------------------------------------------------------------------
+// Forward point-wise B (frame t): BN0 -> Ihat = nl(x - nl(c_i (alpha I + mu)))
+//   (:162), ig = sig(i_w x + i_u I) (:165), I_t = (1-ig) I + ig Ihat (:166)
+//   [no_inh: I_t = gE (:168)]
+// -------------------------------------------------------------------------
 template <class S>
-__global__ __launch_bounds__(NT, 1) void k_fwd_b(CellArgs<S> a) {
+__global__ __launch_bounds__(PW_NT, 2) void k_pw_fb(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds L = carve<S>(smem);
-  S* tile = (S*)L.tile;
+  const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, t = a.t, T = a.T, B = a.B;
-  float* wscr = L.scr + wave * 1024;
+  const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
+  const int t = a.t, T = a.T, B = a.B;
+  const int y0 = part * PW_NW * PWF_RPP;
+  float* wscr = L.scr + wave * SCR_FLOATS;
   const size_t fs = fr_off(1, B), cb = clip_off(b);
 
   if (!a.no_inh) {
-    stage_x(a.x, L.xs, b, t, T, tid);
+    stage_x(a.x, L.xs, b, t, T, y0, PW_NW * PWF_RPP, tid, PW_NT);
     bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * 96, B, a.eps, L.stat,
-                    b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
+                    blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   }
-  tile_zero<S>(tile, tid);
   __syncthreads();
+  if (a.ablate & 4) return;
 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
   const float m0 = L.stat[c], rs0 = L.stat[32 + c];
   const float bi = a.gb[2][c] + a.gb[3][c];
 
-  for (int i = 0; i < RPW; ++i) {
-    const int y = wave * RPW + i;
+#pragma unroll 1
+  for (int i = 0; i < PWF_RPP; ++i) {
+    const int yl = wave * PWF_RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 In;
     if (!a.no_inh) {
       const f32x16 civ = load_cl(a.ci + t * fs + ro, c, h);
       const f32x16 Iv = t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16();
       f32x16 z, xv, ih;
-      stem_cl(L.xs, y, h, st, a.act, z, xv);
+      stem_cl(L.xs, yl, h, st, a.act, z, xv);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float cn = bw0 * ((civ[r] - m0) * rs0) + bb0;
@@ -383,96 +536,59 @@ __global__ __launch_bounds__(NT, 1) void k_fwd_b(CellArgs<S> a) {
     }
     store_cl(a.I + t * fs + ro, c, h, In);
   }
-
-  f32x16 acc[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) acc[i] = zero16();
-  conv_run<S>(acc, a.I + t * fs + cb, a.wf_exc, tile, a.K, wave * RPW, tid, lane);
-#pragma unroll
-  for (int i = 0; i < RPW; ++i)
-    store_cl(a.ce + t * fs + cb + (size_t)(wave * RPW + i) * IMG * C, c, h, acc[i]);
-  bn_fwd_partial(acc, L.red, a.bnacc + ((size_t)t * 2 + 1) * 96, lane, wave, tid);
 }
 
-// =========================================================================
-// Backward A (t from T-1 down to -1).  Two halves:
-//  tail (frame tt = t+1, if tt <= T-1): BN0 backward -> dci (saved for the
-//     w_inh gradient), dgE = conv^T(dci, w_inh) + e_u^T d_e_pre (from k_bwd_b),
-//     attention gate backward (a_w, a_u grads), dE_t complete, dx_{tt} complete
-//     -> stem gradients.
+// -------------------------------------------------------------------------
+// Backward point-wise A (t from T-1 down to -1).  Two halves:
+//  tail (frame tt = t+1, if tt <= T-1): dgE (= conv^T(dci, w_inh) + e_u^T d_e_pre,
+//     prepared by k_conv), attention-gate backward (a_w, a_u grads),
+//     dE_t complete, dx_tt complete -> stem gradients.
 //  head (frame t, if t >= 0): with dE_t: excitation update backward
-//     (:175, :173) -> d_eg, dc_e (-> BN1 bwd partials), kappa/gamma grads,
+//     (:175, :173) -> d_eg, dc_e (-> BN1 bwd sums), kappa/gamma grads,
 //     dI_t (local), dE_{t-1} partial = (1-eg) dE_t.
-// =========================================================================
+// -------------------------------------------------------------------------
 template <class S>
-__global__ __launch_bounds__(NT, 1) void k_bwd_a(CellArgs<S> a) {
+__global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds L = carve<S>(smem);
-  S* tile = (S*)L.tile;
+  const PLds L = pcarve<PWB_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, t = a.t, T = a.T, B = a.B;
-  float* wscr = L.scr + wave * 1024;
+  const int b = blockIdx.x / PWB_WGPC, part = blockIdx.x % PWB_WGPC;
+  const int t = a.t, T = a.T, B = a.B;
+  const int y0 = part * PW_NW * PWB_RPP;
+  float* wscr = L.scr + wave * SCR_FLOATS;
   const size_t fs = fr_off(1, B), cb = clip_off(b);
   const int tt = t + 1;
   const bool tail = tt <= T - 1, head = t >= 0;
-  const bool conv = tail && head && !a.no_inh;   // E_{-1} = 0 makes the frame-0 conv^T dead
-  float* slab_b = a.slab + (size_t)b * SLAB;
+  float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
-  if (tail) {
-    stage_x(a.x, L.xs, b, tt, T, tid);
-    if (!a.no_inh) bn_bwd_finalize(a.bnbacc + ((size_t)tt * 2 + 0) * 64, B, L.stat, tid);
-  }
-  if (conv) tile_zero<S>(tile, tid);
+  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWB_RPP, tid, PW_NT);
+  gacc_zero(L.gacc, 2, tid);
   __syncthreads();
 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   float sm[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int slots[9] = {SM_GBA, SM_KAPPA, SM_GAMMA, SM_BN1W, SM_BN1B, SM_PW0, SM_PW1, SM_PW2, SM_PB};
-  f32x16 gaw = zero16(), gau = zero16();
   float bs0 = 0.f, bs1 = 0.f;   // BN1 bwd partial sums
-
-  f32x16 acc[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) acc[i] = zero16();
-
-  if (tail && !a.no_inh) {
-    const float* bs = a.bnstat + (size_t)tt * 128;
-    const float m0 = bs[c], rs0 = bs[32 + c], bw0 = a.bnw0[c];
-    const float md = L.stat[c], mdx = L.stat[32 + c];
-    for (int i = 0; i < RPW; ++i) {
-      const int y = wave * RPW + i;
-      const size_t ro = cb + (size_t)y * IMG * C;
-      const f32x16 dcv = load_cl(a.dcI + ro, c, h);
-      const f32x16 civ = load_cl(a.ci + tt * fs + ro, c, h);
-      f32x16 v;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float xh = (civ[r] - m0) * rs0;
-        v[r] = rs0 * bw0 * (dcv[r] - md - xh * mdx);
-      }
-      store_cl(a.dci_s + tt * fs + ro, c, h, v);
-    }
-    if (conv) conv_run<S>(acc, a.dci_s + tt * fs + cb, a.wt_inh, tile, a.K, wave * RPW, tid, lane);
-  }
 
   const float ba = a.gb[0][c] + a.gb[1][c];
   const float kap = a.kappa[c], gam = a.gamma[c], bw1 = a.bnw1[c], bb1 = a.bnb1[c];
   float m1 = 0.f, rs1 = 0.f;
   if (head) { m1 = a.bnstat[(size_t)t * 128 + 64 + c]; rs1 = a.bnstat[(size_t)t * 128 + 96 + c]; }
+  const S* dgsrc = a.conv_done ? a.dgE : a.dgEp;
 
-  for (int i = 0; i < RPW; ++i) {
-    const int y = wave * RPW + i;
+#pragma unroll 1
+  for (int i = 0; i < PWB_RPP && !(a.ablate & 4); ++i) {
+    const int yl = wave * PWB_RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 GE;
     if (tail) {
       f32x16 z, xv;
-      stem_cl(L.xs, y, h, st, a.act, z, xv);
+      stem_cl(L.xs, yl, h, st, a.act, z, xv);
       f32x16 dx = load_cl(a.dxp + ro, c, h);
       if (head) {
-        f32x16 dgE = load_cl(a.dgEp + ro, c, h);
-        if (conv) dgE += acc[0];
+        const f32x16 dgE = load_cl(dgsrc + ro, c, h);
         const f32x16 Et = load_cl(a.E + t * fs + ro, c, h);
         F pax[Tr<S>::KS], pae[Tr<S>::KS];
         cl_to_pa<S>(wscr, xv, lane, pax);
@@ -487,8 +603,8 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_a(CellArgs<S> a) {
           dap[r] = dgE[r] * Et[r] * att[r] * (1.f - att[r]);
           sm[0] += dap[r];
         }
-        gaw = wgrad_cl<S>(dap, xv, gaw);
-        gau = wgrad_cl<S>(dap, Et, gau);
+        gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
+        gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
         F pad[Tr<S>::KS];
         cl_to_pa<S>(wscr, dap, lane, pad);
         GE = load_cl(a.dEn + ro, c, h);
@@ -499,7 +615,7 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_a(CellArgs<S> a) {
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const f32x4 xin = L.xs[y * IMG + cl_x(r, h)];
+        const f32x4 xin = L.xs[yl * IMG + cl_x(r, h)];
         const float dz = dx[r] * act_d(z[r], a.act);
         sm[5] += dz * xin[0]; sm[6] += dz * xin[1]; sm[7] += dz * xin[2]; sm[8] += dz;
       }
@@ -537,164 +653,230 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_a(CellArgs<S> a) {
       store_cl(a.dEp + ro, c, h, dEp);
       store_cl(a.dcE + ro, c, h, dcE);
     }
-    shift_rows(acc);
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
-  if (head) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * 64, lane, wave, tid);
-  flush_small<9>(sm, slots, L.small, slab_b, lane, wave, tid);
-  if (tail && head) {
-    flush_gate(gaw, L.scr, slab_b + 0 * 1024, lane, wave, tid);
-    flush_gate(gau, L.scr, slab_b + 1 * 1024, lane, wave, tid);
-  }
+  if (head && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * 64, lane, wave, tid);
+  if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, slab_p, lane, wave, tid);   // ends with a barrier
+  if (tail && head && !(a.ablate & 32)) gacc_flush(L.gacc, slab_p, 0, 2, tid);
 }
 
-// =========================================================================
-// Backward B (frame t): BN1 backward -> dce (saved for the w_exc gradient),
-//   dI_t = conv^T(dce, w_exc) + local + from frame t+1;
-//   inhibition update backward (:166, :165, :162) -> i_w/i_u, alpha, mu,
-//   dc_i (-> BN0 bwd partials), dx_t partial, dI_{t-1};
-//   exc gate backward (:171) -> e_w/e_u grads, dI_{t-1}, dgE partial.
-// =========================================================================
+// -------------------------------------------------------------------------
+// Backward point-wise B (frame t): with dI_t (= conv^T(dce, w_exc) + local
+//   + from frame t+1, prepared by k_conv): inhibition update backward
+//   (:166, :165, :162) -> i_w/i_u, alpha, mu, dc_i (-> BN0 bwd sums),
+//   dx_t partial, dI_{t-1}; exc gate backward (:171) -> e_w/e_u grads,
+//   dI_{t-1}, dgE partial.
+// -------------------------------------------------------------------------
 template <class S>
-__global__ __launch_bounds__(NT, 1) void k_bwd_b(CellArgs<S> a) {
+__global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds L = carve<S>(smem);
-  S* tile = (S*)L.tile;
+  const PLds L = pcarve<PWB_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, t = a.t, T = a.T, B = a.B;
-  float* wscr = L.scr + wave * 1024;
+  const int b = blockIdx.x / PWB_WGPC, part = blockIdx.x % PWB_WGPC;
+  const int t = a.t, T = a.T, B = a.B;
+  const int y0 = part * PW_NW * PWB_RPP;
+  float* wscr = L.scr + wave * SCR_FLOATS;
   const size_t fs = fr_off(1, B), cb = clip_off(b);
-  float* slab_b = a.slab + (size_t)b * SLAB;
+  float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
-  stage_x(a.x, L.xs, b, t, T, tid);
-  bn_bwd_finalize(a.bnbacc + ((size_t)t * 2 + 1) * 64, B, L.stat, tid);
-  tile_zero<S>(tile, tid);
+  stage_x(a.x, L.xs, b, t, T, y0, PW_NW * PWB_RPP, tid, PW_NT);
+  gacc_zero(L.gacc, 4, tid);
   __syncthreads();
 
   const float* bs = a.bnstat + (size_t)t * 128;
-  {
-    const float m1 = bs[64 + c], rs1 = bs[96 + c], bw1 = a.bnw1[c];
-    const float md = L.stat[c], mdx = L.stat[32 + c];
-    for (int i = 0; i < RPW; ++i) {
-      const int y = wave * RPW + i;
-      const size_t ro = cb + (size_t)y * IMG * C;
-      const f32x16 dcv = load_cl(a.dcE + ro, c, h);
-      const f32x16 cev = load_cl(a.ce + t * fs + ro, c, h);
-      f32x16 v;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float xh = (cev[r] - m1) * rs1;
-        v[r] = rs1 * bw1 * (dcv[r] - md - xh * mdx);
-      }
-      store_cl(a.dce_s + t * fs + ro, c, h, v);
-    }
-  }
-  f32x16 acc[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) acc[i] = zero16();
-  conv_run<S>(acc, a.dce_s + t * fs + cb, a.wt_exc, tile, a.K, wave * RPW, tid, lane);
-
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
   const float m0 = bs[c], rs0 = bs[32 + c];
   const float bi = a.gb[2][c] + a.gb[3][c];
-  float sm[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int slots[7] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B, SM_GBA};
-  f32x16 giw = zero16(), giu = zero16(), gew = zero16(), geu = zero16();
+  float sm[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int slots[6] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B};
   float bs0 = 0.f, bs1 = 0.f;
 
-  for (int i = 0; i < RPW; ++i) {
-    const int y = wave * RPW + i;
+#pragma unroll 1
+  for (int i = 0; i < PWB_RPP && !(a.ablate & 4); ++i) {
+    const int yl = wave * PWB_RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
-    f32x16 dIt = acc[0] + load_cl(a.dIl + ro, c, h);
-    if (t < T - 1 && !a.no_inh) dIt += load_cl(a.GI + ro, c, h);
-    const f32x16 dep = load_cl(a.dEp + ro, c, h);
-    const f32x16 gEv = load_cl(a.gE + t * fs + ro, c, h);
-    if (!a.no_inh) {
-      const f32x16 Iv = t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16();
-      const f32x16 civ = load_cl(a.ci + t * fs + ro, c, h);
-      f32x16 z, xv;
-      stem_cl(L.xs, y, h, st, a.act, z, xv);
-      F pax[Tr<S>::KS], pai[Tr<S>::KS];
-      cl_to_pa<S>(wscr, xv, lane, pax);
-      cl_to_pa<S>(wscr, Iv, lane, pai);
-      f32x16 g = zero16();
-      g = gemm_pa<S>(pax, a.gf[2], g, lane);
-      g = gemm_pa<S>(pai, a.gf[3], g, lane);
-      f32x16 dIp, dip, dx, dci;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float xi = (civ[r] - m0) * rs0;
-        const float cn = bw0 * xi + bb0;
-        const float u = al * Iv[r] + mu;
-        const float p = cn * u;
-        const float q = xv[r] - act_f(p, a.act);
-        const float ih = act_f(q, a.act);
-        const float ig = sigm(g[r] + bi);
-        const float dih = dIt[r] * ig;
-        dip[r] = dIt[r] * (ih - Iv[r]) * ig * (1.f - ig);
-        const float dq = dih * act_d(q, a.act);
-        const float dp = -dq * act_d(p, a.act);
-        const float du = dp * cn;
-        dci[r] = dp * u;
-        dx[r] = dq;
-        dIp[r] = dIt[r] * (1.f - ig) + du * al;
-        sm[0] += du * Iv[r];
-        sm[1] += du;
-        sm[2] += dip[r];
-        bs0 += dci[r];
-        bs1 += dci[r] * xi;
-      }
-      giw = wgrad_cl<S>(dip, xv, giw);
-      giu = wgrad_cl<S>(dip, Iv, giu);
-      F pd[Tr<S>::KS];
-      cl_to_pa<S>(wscr, dip, lane, pd);
-      dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
-      dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
-      // exc gate: eg = sig(e_w I_{t-1} + e_u gE)
-      gew = wgrad_cl<S>(dep, Iv, gew);
-      geu = wgrad_cl<S>(dep, gEv, geu);
-      F pe[Tr<S>::KS];
-      cl_to_pa<S>(wscr, dep, lane, pe);
-      dIp = gemm_pa<S>(pe, a.gt[4], dIp, lane);
-      const f32x16 dg = gemm_pa<S>(pe, a.gt[5], zero16(), lane);
+    // exc gate first (:171): eg = sig(e_w g_inh + e_u gE), g_inh = I_{t-1} (InT) / E_{t-1} (no_inh)
+    f32x16 eI;       // e_w^T d_e_pre, a dI_{t-1} (InT) or dE_{t-1} (no_inh) contribution
+    const f32x16 ginh = a.no_inh ? (t > 0 ? load_cl(a.E + (t - 1) * fs + ro, c, h) : zero16())
+                                 : (t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16());
+    {
+      const f32x16 dep = load_cl(a.dEp + ro, c, h);
+      const f32x16 gEv = load_cl(a.gE + t * fs + ro, c, h);
+      gacc_row<S>(L.gacc + 2 * 1024, L.flush, dep, ginh, lane, wave, tid);
+      gacc_row<S>(L.gacc + 3 * 1024, L.flush, dep, gEv, lane, wave, tid);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sm[3] += dep[r];
-      store_cl(a.dcI + ro, c, h, dci);
-      store_cl(a.GI + ro, c, h, dIp);
-      store_cl(a.dxp + ro, c, h, dx);
-      store_cl(a.dgEp + ro, c, h, dg);
-    } else {
-      // no_inh (:168): I_t = gE_t, eg = sig(e_w E_{t-1} + e_u gE_t)
-      const f32x16 Ep = t > 0 ? load_cl(a.E + (t - 1) * fs + ro, c, h) : zero16();
-      gew = wgrad_cl<S>(dep, Ep, gew);
-      geu = wgrad_cl<S>(dep, gEv, geu);
       F pe[Tr<S>::KS];
       cl_to_pa<S>(wscr, dep, lane, pe);
-      f32x16 dEn = load_cl(a.dEn + ro, c, h);
-      dEn = gemm_pa<S>(pe, a.gt[4], dEn, lane);
-      const f32x16 dg = gemm_pa<S>(pe, a.gt[5], dIt, lane);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sm[3] += dep[r];
-      store_cl(a.dEn + ro, c, h, dEn);
+      eI = gemm_pa<S>(pe, a.gt[4], zero16(), lane);
+      const f32x16 dIt0 = a.no_inh ? load_cl(a.dIt + ro, c, h) : zero16();
+      const f32x16 dg = gemm_pa<S>(pe, a.gt[5], dIt0, lane);   // no_inh: I_t = gE_t
       store_cl(a.dgEp + ro, c, h, dg);
-      store_cl(a.dxp + ro, c, h, zero16());
     }
-    shift_rows(acc);
+    if (a.no_inh) {
+      f32x16 dEn = load_cl(a.dEn + ro, c, h);
+      dEn += eI;
+      store_cl(a.dEn + ro, c, h, dEn);
+      store_cl(a.dxp + ro, c, h, zero16());
+      continue;
+    }
+    const f32x16 Iv = ginh;
+    const f32x16 dIt = load_cl(a.dIt + ro, c, h);
+    const f32x16 civ = load_cl(a.ci + t * fs + ro, c, h);
+    f32x16 z, xv;
+    stem_cl(L.xs, yl, h, st, a.act, z, xv);
+    F pax[Tr<S>::KS], pai[Tr<S>::KS];
+    cl_to_pa<S>(wscr, xv, lane, pax);
+    cl_to_pa<S>(wscr, Iv, lane, pai);
+    f32x16 g = zero16();
+    g = gemm_pa<S>(pax, a.gf[2], g, lane);
+    g = gemm_pa<S>(pai, a.gf[3], g, lane);
+    f32x16 dIp, dip, dx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float xi = (civ[r] - m0) * rs0;
+      const float cn = bw0 * xi + bb0;
+      const float u = al * Iv[r] + mu;
+      const float p = cn * u;
+      const float q = xv[r] - act_f(p, a.act);
+      const float ih = act_f(q, a.act);
+      const float ig = sigm(g[r] + bi);
+      const float dih = dIt[r] * ig;
+      dip[r] = dIt[r] * (ih - Iv[r]) * ig * (1.f - ig);
+      const float dq = dih * act_d(q, a.act);
+      const float dp = -dq * act_d(p, a.act);
+      const float du = dp * cn;
+      const float dci = dp * u;
+      stf(a.dcI + ro + cl_x(r, h) * C + c, dci);
+      dx[r] = dq;
+      dIp[r] = dIt[r] * (1.f - ig) + du * al + eI[r];
+      sm[0] += du * Iv[r];
+      sm[1] += du;
+      sm[2] += dip[r];
+      bs0 += dci;
+      bs1 += dci * xi;
+    }
+    gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
+    gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, Iv, lane, wave, tid);
+    F pd[Tr<S>::KS];
+    cl_to_pa<S>(wscr, dip, lane, pd);
+    dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
+    dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
+    store_cl(a.GI + ro, c, h, dIp);
+    store_cl(a.dxp + ro, c, h, dx);
   }
   sm[4] = bs1;
   sm[5] = bs0;
-  if (!a.no_inh) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * 64, lane, wave, tid);
-  flush_small<7>(sm, slots, L.small, slab_b, lane, wave, tid);
-  if (!a.no_inh) {
-    flush_gate(giw, L.scr, slab_b + 2 * 1024, lane, wave, tid);
-    flush_gate(giu, L.scr, slab_b + 3 * 1024, lane, wave, tid);
+  if (!a.no_inh && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * 64, lane, wave, tid);
+  if (a.ablate & 32) return;
+  flush_small<6>(sm, slots, L.small, slab_p, lane, wave, tid);   // ends with a barrier
+  // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5
+  if (!a.no_inh) gacc_flush(L.gacc, slab_p, 2, 2, tid);
+  gacc_flush(L.gacc + 2 * 1024, slab_p, 4, 2, tid);
+}
+
+constexpr int WG_RB = 8;               // D rows per band
+constexpr int WG_XR = WG_RB + 2 * PADMAX;
+constexpr int WG_NACC = 13;            // taps per wave: wave + 4 m, m < 13
+template <class S>
+constexpr int wgrad_lds_bytes() {
+  return (WG_XR * TILE * C + WG_RB * IMG * C) * (int)sizeof(S);
+}
+
+// Unswizzled channels-last band images: the transposed 4x16 block reads
+// (ds_read_b64_tr_b16) and the f32 row reads are bank-conflict free on them,
+// and every tap is a constant element offset from a per-lane base.
+__device__ __forceinline__ int wx_off(int row, int col, int ch) { return (row * TILE + col) * C + ch; }
+__device__ __forceinline__ int wd_off(int row, int col, int ch) { return (row * IMG + col) * C + ch; }
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+__device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
+}
+
+template <class S, int K>
+__device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __restrict__ Xs,
+                                          const S* __restrict__ Ds, int B, int T, int g, int nwg,
+                                          S* xt, S* dt, int tid, int lane, int wave, int ablate) {
+  constexpr int KK = K * K;
+  constexpr int off = PADMAX - K / 2;
+  constexpr int CPB = 16 / (int)sizeof(S);
+  constexpr int NCH = C / CPB;
+  // wave-uniform element offset of each tap; taps beyond K*K (the 13th slot of
+  // waves 1-3 at K=7) read tap 0 and their accumulator is never stored, so
+  // every MFMA is unconditional (no accumulator copies around branches)
+  int toff[WG_NACC];
+#pragma unroll
+  for (int m = 0; m < WG_NACC; ++m) {
+    const int tap = wave + 4 * m < KK ? wave + 4 * m : 0;
+    const int kh = tap / K, kw = tap - kh * K;
+    toff[m] = (kh * TILE + kw) * C;
   }
-  flush_gate(gew, L.scr, slab_b + 4 * 1024, lane, wave, tid);
-  flush_gate(geu, L.scr, slab_b + 5 * 1024, lane, wave, tid);
+  for (int f = g; f < B * T; f += nwg) {
+    const int t = f / B, b = f % B;
+    const S* xsrc = Xs + ((size_t)t * B + b) * NPIX * C;
+    const S* dsrc = Ds + ((size_t)t * B + b) * NPIX * C;
+    for (int y0 = 0; y0 < IMG; y0 += WG_RB) {
+      __syncthreads();
+      // X band: image rows y0-3 .. y0+RB+2, padded columns, zero outside
+      for (int idx = tid; idx < WG_XR * TILE * NCH && !(ablate & 128); idx += NT) {
+        const int q = idx % NCH, pc = idx / NCH;
+        const int col = pc % TILE, row = pc / TILE;
+        const int iy = y0 + row - PADMAX, ix = col - PADMAX;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (iy >= 0 && iy < IMG && ix >= 0 && ix < IMG)
+          v = *(const uint4*)(xsrc + (iy * IMG + ix) * C + q * CPB);
+        *(uint4*)(xt + wx_off(row, col, q * CPB)) = v;
+      }
+      for (int idx = tid; idx < WG_RB * IMG * NCH && !(ablate & 128); idx += NT) {
+        const int q = idx % NCH, pc = idx / NCH;
+        *(uint4*)(dt + pc * C + q * CPB) = *(const uint4*)(dsrc + (y0 * IMG + pc) * C + q * CPB);
+      }
+      __syncthreads();
+      if (ablate & 64) continue;
+      if constexpr (sizeof(S) == 4) {
+        // k-step = 2 pixels (x0 + h); lane&31 is ci for A, n for B
+        const int ch = lane & 31, h = lane >> 5;
+        for (int yd = 0; yd < WG_RB; ++yd) {
+          const int xb = wx_off(yd + off, h + off, ch), db = wd_off(yd, h, ch);
+          for (int x0 = 0; x0 < IMG; x0 += 2) {
+            const float bv = dt[db + x0 * C];
+#pragma unroll
+            for (int m = 0; m < WG_NACC; ++m) {
+              const float av = xt[xb + x0 * C + toff[m]];
+              acc[m] = Tr<float>::mma(av, bv, acc[m]);
+            }
+          }
+        }
+      } else {
+        // k-step = 16 pixels.  Lane 4q+p' of each 16-lane group addresses pixel
+        // (x0 + 8 hh + q [+4]) and channels 16 (grp&1) + 4p' .. +3.
+        const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
+        const int chb = 16 * (grp & 1) + 4 * pp;
+        const int hh = grp >> 1;
+        for (int yd = 0; yd < WG_RB; ++yd) {
+          for (int x0 = 0; x0 < IMG; x0 += 16) {
+            const int dc0 = x0 + 8 * hh + q;
+            const bf16_t* dp = (const bf16_t*)dt + wd_off(yd, dc0, chb);
+            const bf16x8 bv = __builtin_shufflevector(tr_read(dp), tr_read(dp + 4 * C),
+                                                      0, 1, 2, 3, 4, 5, 6, 7);
+            const bf16_t* xp = (const bf16_t*)xt + wx_off(yd + off, dc0 + off, chb);
+#pragma unroll
+            for (int m = 0; m < WG_NACC; ++m) {
+              const bf16_t* ap = xp + toff[m];
+              const bf16x8 av = __builtin_shufflevector(tr_read(ap), tr_read(ap + 4 * C),
+                                                        0, 1, 2, 3, 4, 5, 6, 7);
+              acc[m] = Tr<bf16_t>::mma(av, bv, acc[m]);
+            }
+          }
+        }
+      }
+    }
+  }
 }
 
 // =========================================================================
@@ -704,122 +886,26 @@ __global__ __launch_bounds__(NT, 1) void k_bwd_b(CellArgs<S> a) {
 // Each wave owns taps {w, w+4, ...} (<= 13 32x32 accumulator tiles); the
 // D / X row bands are staged in LDS; per-workgroup partials go to wslab.
 // =========================================================================
-constexpr int WG_RB = 8;               // D rows per band
-constexpr int WG_XR = WG_RB + 2 * PADMAX;
-constexpr int WG_NACC = 13;
 template <class S>
-constexpr int wgrad_lds_bytes() {
-  return (WG_XR * TILE * C + WG_RB * IMG * C) * (int)sizeof(S);
-}
-
-template <class S>
-__device__ __forceinline__ int wx_off(int row, int col, int ch) {   // X band image
-  if constexpr (sizeof(S) == 4) return (row * TILE + col) * C + ch;
-  else return (row * TILE + col) * C + ((((ch >> 3) ^ ((col >> 2) & 3))) << 3) + (ch & 7);
-}
-template <class S>
-__device__ __forceinline__ int wd_off(int row, int col, int ch) {   // D band image
-  if constexpr (sizeof(S) == 4) return (row * IMG + col) * C + ch;
-  else return (row * IMG + col) * C + ((((ch >> 3) ^ ((col >> 2) & 3))) << 3) + (ch & 7);
-}
-
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-__device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
-}
-
-template <class S>
-__global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, int nwg) {
+__global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, int nwg, int conv0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   S* xt = (S*)smem;
   S* dt = xt + WG_XR * TILE * C;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = blockIdx.x, conv = blockIdx.y;
-  const int K = a.K, KK = K * K, off = PADMAX - K / 2;
-  const int B = a.B, T = a.T;
+  const int g = blockIdx.x, conv = blockIdx.y + conv0;
+  const int KK = a.K * a.K;
   const S* Xs = conv == 0 ? a.gE : a.I;
   const S* Ds = conv == 0 ? a.dci_s : a.dce_s;
-  constexpr int CPB = 16 / (int)sizeof(S);
-  constexpr int NCH = C / CPB;
 
   f32x16 acc[WG_NACC];
 #pragma unroll
   for (int m = 0; m < WG_NACC; ++m) acc[m] = zero16();
-
-  for (int f = g; f < B * T; f += nwg) {
-    const int t = f / B, b = f % B;
-    const S* xsrc = Xs + ((size_t)t * B + b) * NPIX * C;
-    const S* dsrc = Ds + ((size_t)t * B + b) * NPIX * C;
-    for (int y0 = 0; y0 < IMG; y0 += WG_RB) {
-      __syncthreads();
-      // X band: image rows y0-3 .. y0+RB+2, padded columns, zero outside
-      for (int idx = tid; idx < WG_XR * TILE * NCH; idx += NT) {
-        const int q = idx % NCH, pc = idx / NCH;
-        const int col = pc % TILE, row = pc / TILE;
-        const int iy = y0 + row - PADMAX, ix = col - PADMAX;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (iy >= 0 && iy < IMG && ix >= 0 && ix < IMG)
-          v = *(const uint4*)(xsrc + (iy * IMG + ix) * C + q * CPB);
-        *(uint4*)(xt + wx_off<S>(row, col, q * CPB)) = v;
-      }
-      for (int idx = tid; idx < WG_RB * IMG * NCH; idx += NT) {
-        const int q = idx % NCH, pc = idx / NCH;
-        const int col = pc % IMG, row = pc / IMG;
-        *(uint4*)(dt + wd_off<S>(row, col, q * CPB)) =
-            *(const uint4*)(dsrc + ((y0 + row) * IMG + col) * C + q * CPB);
-      }
-      __syncthreads();
-      if constexpr (sizeof(S) == 4) {
-        // f32: k-step = 2 pixels (x0 + h), lane (col = l&31) is ci for A, n for B
-        const int ch = lane & 31;
-        for (int yd = 0; yd < WG_RB; ++yd) {
-          for (int x0 = 0; x0 < IMG; x0 += 2) {
-            const float bv = dt[wd_off<S>(yd, x0 + h, ch)];
-#pragma unroll
-            for (int m = 0; m < WG_NACC; ++m) {
-              const int tap = wave + 4 * m;
-              if (tap < KK) {
-                const int kh = tap / K, kw = tap - kh * K;
-                const float av = xt[wx_off<S>(yd + kh + off, x0 + h + kw + off, ch)];
-                acc[m] = Tr<float>::mma(av, bv, acc[m]);
-              }
-            }
-          }
-        }
-      } else {
-        // bf16: k-step = 16 pixels; fragments by ds_read_b64_tr_b16 from the
-        // channels-last images (lane 4q+p' addresses pixel q, channels 4p'..4p'+3
-        // of its 16-lane group's channel half).
-        const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
-        const int chb = 16 * (grp & 1) + 4 * pp;
-        const int hh = grp >> 1;
-        for (int yd = 0; yd < WG_RB; ++yd) {
-          for (int x0 = 0; x0 < IMG; x0 += 16) {
-            const int dc0 = x0 + 8 * hh + q;
-            const bf16x4 b0 = tr_read((const bf16_t*)dt + wd_off<S>(yd, dc0, chb));
-            const bf16x4 b1 = tr_read((const bf16_t*)dt + wd_off<S>(yd, dc0 + 4, chb));
-            bf16x8 bv;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) { bv[j] = b0[j]; bv[4 + j] = b1[j]; }
-#pragma unroll
-            for (int m = 0; m < WG_NACC; ++m) {
-              const int tap = wave + 4 * m;
-              if (tap < KK) {
-                const int kh = tap / K, kw = tap - kh * K;
-                const int tr = yd + kh + off, tc = dc0 + kw + off;
-                const bf16x4 a0 = tr_read((const bf16_t*)xt + wx_off<S>(tr, tc, chb));
-                const bf16x4 a1 = tr_read((const bf16_t*)xt + wx_off<S>(tr, tc + 4, chb));
-                bf16x8 av;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) { av[j] = a0[j]; av[4 + j] = a1[j]; }
-                acc[m] = Tr<bf16_t>::mma(av, bv, acc[m]);
-              }
-            }
-          }
-        }
-      }
-    }
+  switch (a.K) {
+    case 7: wgrad_run<S, 7>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
+    case 5: wgrad_run<S, 5>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
+    case 3: wgrad_run<S, 3>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
+    default: wgrad_run<S, 1>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
   }
   // acc[m]: rows ci = cl_x(r,h), cols n = lane&31
   float* dst = wslab + ((size_t)conv * nwg + g) * MAXTAP * 1024;
@@ -1023,7 +1109,7 @@ struct Plan {
   // saved offsets
   size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_bnstat, o_wf[4], o_g[12], saved;
   // workspace offsets
-  size_t o_bnacc, o_bnbacc, o_tr[9], o_dci, o_dce, o_slab, o_wslab, ws;
+  size_t o_bnacc, o_bnbacc, o_tr[NTRANS], o_dci, o_dce, o_slab, o_wslab, ws;
   int nwg;
 };
 
@@ -1061,10 +1147,10 @@ Plan plan(const pt_cell_desc* d) {
   o = 0;
   p.o_bnacc = o; o += al((size_t)p.T * 2 * 96 * 8);
   p.o_bnbacc = o; o += al((size_t)p.T * 2 * 64 * 8);
-  for (int i = 0; i < 9; ++i) { p.o_tr[i] = o; o += al(p.frame * 4); }
+  for (int i = 0; i < NTRANS; ++i) { p.o_tr[i] = o; o += al(p.frame * 4); }   // GEfin f32
   p.o_dci = o; o += fbytes;
   p.o_dce = o; o += fbytes;
-  p.o_slab = o; o += al((size_t)p.B * SLAB * 4);
+  p.o_slab = o; o += al((size_t)p.B * PW_PARTS * SLAB * 4);
   p.nwg = p.B * p.T < 256 ? p.B * p.T : 256;
   p.o_wslab = o; o += al((size_t)2 * p.nwg * MAXTAP * 1024 * 4);
   p.ws = o;
@@ -1078,6 +1164,10 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
   memset(&a, 0, sizeof(a));
   a.B = p.B; a.T = p.T; a.K = p.K; a.act = d->act; a.no_inh = d->no_inh; a.eps = d->eps;
   a.x = x;
+  {
+    const char* ab = getenv("PT_CELL_ABLATE");     // timing experiments only
+    a.ablate = ab ? atoi(ab) : 0;
+  }
   a.wpre = pr->preproc_w; a.bpre = pr->preproc_b;
   a.alpha = pr->alpha; a.mu = pr->mu; a.gamma = pr->gamma; a.kappa = pr->kappa;
   a.bnw0 = pr->bn_w[0]; a.bnb0 = pr->bn_b[0]; a.bnw1 = pr->bn_w[1]; a.bnb1 = pr->bn_b[1];
@@ -1094,9 +1184,10 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
   if (ws) {
     a.bnacc = (double*)(ws + p.o_bnacc);
     a.bnbacc = (double*)(ws + p.o_bnbacc);
-    float** tr[9] = {&a.dEn, &a.dcE, &a.dIl, &a.dEp, &a.dcI, &a.GI, &a.dgEp, &a.dxp, nullptr};
-    for (int i = 0; i < 8; ++i) *tr[i] = (float*)(ws + p.o_tr[i]);
-    a.GEfin = (const float*)(ws + p.o_tr[8]);
+    S** tr[NTRANS] = {&a.dEn, &a.dcE, &a.dIl, &a.dEp, &a.dcI, &a.GI, &a.dgEp, &a.dxp,
+                      &a.dgE, &a.dIt, nullptr};
+    for (int i = 0; i < NTRANS - 1; ++i) *tr[i] = (S*)(ws + p.o_tr[i]);
+    a.GEfin = (const float*)(ws + p.o_tr[NTRANS - 1]);
     a.dci_s = (S*)(ws + p.o_dci); a.dce_s = (S*)(ws + p.o_dce);
     a.slab = (float*)(ws + p.o_slab);
   }
@@ -1108,17 +1199,31 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
     if (e_ != hipSuccess) return fail(PT_ERR_HIP, "HIP error %s at line %ld", hipGetErrorString(e_), __LINE__); \
   } while (0)
 
+#define SETLDS(kern, bytes) \
+  HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
+
 template <class S>
 int set_lds_attrs() {
   static thread_local bool done = false;   // per host thread; cheap either way
   if (done) return 0;
-  HIPCHK(hipFuncSetAttribute((const void*)k_fwd_a<S>, hipFuncAttributeMaxDynamicSharedMemorySize, cell_lds_bytes<S>()));
-  HIPCHK(hipFuncSetAttribute((const void*)k_fwd_b<S>, hipFuncAttributeMaxDynamicSharedMemorySize, cell_lds_bytes<S>()));
-  HIPCHK(hipFuncSetAttribute((const void*)k_bwd_a<S>, hipFuncAttributeMaxDynamicSharedMemorySize, cell_lds_bytes<S>()));
-  HIPCHK(hipFuncSetAttribute((const void*)k_bwd_b<S>, hipFuncAttributeMaxDynamicSharedMemorySize, cell_lds_bytes<S>()));
-  HIPCHK(hipFuncSetAttribute((const void*)k_wgrad<S>, hipFuncAttributeMaxDynamicSharedMemorySize, wgrad_lds_bytes<S>()));
+  SETLDS((k_conv<S, FILL_COPY, EPI_FWD>), conv_lds_bytes<S>());
+  SETLDS((k_conv<S, FILL_BNBWD, EPI_ADD>), conv_lds_bytes<S>());
+  SETLDS((k_conv<S, FILL_BNBWD, EPI_NONE>), conv_lds_bytes<S>());
+  SETLDS(k_pw_fa<S>, pw_lds_bytes<PWF_RPP>());
+  SETLDS(k_pw_fb<S>, pw_lds_bytes<PWF_RPP>());
+  SETLDS(k_pw_ba<S>, pw_lds_bytes<PWB_RPP>());
+  SETLDS(k_pw_bb<S>, pw_lds_bytes<PWB_RPP>());
+  SETLDS(k_wgrad<S>, wgrad_lds_bytes<S>());
   done = true;
   return 0;
+}
+
+template <class S>
+ConvArgs<S> conv_args(const CellArgs<S>& a) {
+  ConvArgs<S> c;
+  memset(&c, 0, sizeof(c));
+  c.B = a.B; c.K = a.K; c.ablate = a.ablate;
+  return c;
 }
 
 template <class S>
@@ -1140,11 +1245,25 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   pa.wt_inh = (S*)((char*)saved + p.o_wf[2]); pa.wt_exc = (S*)((char*)saved + p.o_wf[3]);
   HIPCHK(hipMemsetAsync((char*)ws + p.o_bnacc, 0, (size_t)p.T * 2 * 96 * 8, st));
   timed(PT_K_PREP, st, [&] { hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa); });
-  const size_t lds = cell_lds_bytes<S>();
+  const dim3 gpf(p.B * PWF_WGPC);
+  const size_t lpf = pw_lds_bytes<PWF_RPP>(), lcv = conv_lds_bytes<S>();
+  const size_t fs = p.frame;
+  ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
+  ca.wf = a.wf_inh;
+  cb.wf = a.wf_exc;
   for (int t = 0; t <= p.T; ++t) {
     a.t = t;
-    timed(PT_K_FWD_A, st, [&] { hipLaunchKernelGGL(k_fwd_a<S>, dim3(p.B), dim3(NT), lds, st, a); });
-    if (t < p.T) timed(PT_K_FWD_B, st, [&] { hipLaunchKernelGGL(k_fwd_b<S>, dim3(p.B), dim3(NT), lds, st, a); });
+    timed(PT_K_PW_FA, st, [&] { hipLaunchKernelGGL(k_pw_fa<S>, gpf, dim3(PW_NT), lpf, st, a); });
+    if (t == p.T) break;
+    if (!d->no_inh) {
+      ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * 96;
+      timed(PT_K_CONV_FA, st, [&] {
+        hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, ca); });
+    }
+    timed(PT_K_PW_FB, st, [&] { hipLaunchKernelGGL(k_pw_fb<S>, gpf, dim3(PW_NT), lpf, st, a); });
+    cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * 96;
+    timed(PT_K_CONV_FB, st, [&] {
+      hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, cb); });
   }
   if (e_last)
     hipLaunchKernelGGL(k_to_nchw<S>, dim3(256), dim3(256), 0, st,
@@ -1161,30 +1280,54 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   if (int rc = set_lds_attrs<S>()) return rc;
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
-  HIPCHK(hipMemsetAsync((char*)ws + p.o_slab, 0, (size_t)p.B * SLAB * 4, st));
+  HIPCHK(hipMemsetAsync((char*)ws + p.o_slab, 0, (size_t)p.B * PW_PARTS * SLAB * 4, st));
   HIPCHK(hipMemsetAsync((char*)ws + p.o_bnbacc, 0, (size_t)p.T * 2 * 64 * 8, st));
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
-                     (float*)((char*)ws + p.o_tr[8]), p.B);
-  const size_t lds = cell_lds_bytes<S>();
+                     (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B);
+  const dim3 gpb(p.B * PWB_WGPC);
+  const size_t lpb = pw_lds_bytes<PWB_RPP>(), lcv = conv_lds_bytes<S>();
+  const size_t fs = p.frame;
+  const float* bst = a.bnstat;
   a.t = p.T - 1;
-  timed(PT_K_BWD_A, st, [&] { hipLaunchKernelGGL(k_bwd_a<S>, dim3(p.B), dim3(NT), lds, st, a); });
+  a.conv_done = 0;
+  timed(PT_K_PW_BA, st, [&] { hipLaunchKernelGGL(k_pw_ba<S>, gpb, dim3(PW_NT), lpb, st, a); });
   for (int t = p.T - 1; t >= 0; --t) {
+    // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
+    ConvArgs<S> cb = conv_args(a);
+    cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
+    cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
+    cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
+    timed(PT_K_CONV_BB, st, [&] {
+      hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_ADD>), dim3(p.B), dim3(NT), lcv, st, cb); });
     a.t = t;
-    timed(PT_K_BWD_B, st, [&] { hipLaunchKernelGGL(k_bwd_b<S>, dim3(p.B), dim3(NT), lds, st, a); });
+    timed(PT_K_PW_BB, st, [&] { hipLaunchKernelGGL(k_pw_bb<S>, gpb, dim3(PW_NT), lpb, st, a); });
+    a.conv_done = 0;
+    if (!d->no_inh) {
+      // dgE_t = conv^T(BN0-bwd(dcI), w_inh) + e_u^T d_e_pre ; frame 0's conv^T is dead (E_{-1}=0)
+      ConvArgs<S> ca = conv_args(a);
+      ca.dc = a.dcI; ca.raw = a.ci + t * fs; ca.bnstat = bst + (size_t)t * 128;
+      ca.bnb = a.bnbacc + ((size_t)t * 2 + 0) * 64; ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
+      ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
+      if (t >= 1) {
+        timed(PT_K_CONV_BA, st, [&] {
+          hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_ADD>), dim3(p.B), dim3(NT), lcv, st, ca); });
+        a.conv_done = 1;
+      } else {
+        timed(PT_K_CONV_BA, st, [&] {
+          hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_NONE>), dim3(p.B), dim3(NT), lcv, st, ca); });
+      }
+    }
     a.t = t - 1;
-    timed(PT_K_BWD_A, st, [&] { hipLaunchKernelGGL(k_bwd_a<S>, dim3(p.B), dim3(NT), lds, st, a); });
+    timed(PT_K_PW_BA, st, [&] { hipLaunchKernelGGL(k_pw_ba<S>, gpb, dim3(PW_NT), lpb, st, a); });
   }
   float* wslab = (float*)((char*)ws + p.o_wslab);
-  if (!d->no_inh) {
-    timed(PT_K_WGRAD, st, [&] { hipLaunchKernelGGL(k_wgrad<S>, dim3(p.nwg, 2), dim3(NT), wgrad_lds_bytes<S>(), st, a, wslab, p.nwg); });
-  } else {
-    HIPCHK(hipMemsetAsync(wslab, 0, (size_t)p.nwg * MAXTAP * 1024 * 4, st));
-    // conv 1 only (w_exc); conv 0 slab stays zero
-    CellArgs<S> a2 = a;
-    hipLaunchKernelGGL(k_wgrad<S>, dim3(p.nwg, 2), dim3(NT), wgrad_lds_bytes<S>(), st, a2, wslab, p.nwg);
-  }
+  const int conv0 = d->no_inh ? 1 : 0;
+  if (d->no_inh) HIPCHK(hipMemsetAsync(wslab, 0, (size_t)p.nwg * MAXTAP * 1024 * 4, st));
+  timed(PT_K_WGRAD, st, [&] {
+    hipLaunchKernelGGL(k_wgrad<S>, dim3(p.nwg, 2 - conv0), dim3(NT), wgrad_lds_bytes<S>(), st, a,
+                       wslab, p.nwg, conv0); });
   ReduceArgs r;
-  r.B = p.B; r.K = p.K; r.nwg = p.nwg;
+  r.B = p.B * PW_PARTS; r.K = p.K; r.nwg = p.nwg;
   r.slab = (const float*)((char*)ws + p.o_slab);
   r.wslab = wslab;
   r.g = *g;

@@ -134,12 +134,17 @@ __device__ __forceinline__ float act_d(float x, int act) {   // d nl / d x
 }
 
 // --------------------------------------------------------- per-wave transpose
-// 32x32 f32 scratch, swizzled so the CL write and the PA read are both
-// bank-conflict free for the read width each dtype uses.
-template <class S> __device__ __forceinline__ int scr_idx(int p, int c);
-template <> __device__ __forceinline__ int scr_idx<float>(int p, int c) { return p * 32 + (c ^ p); }
-template <> __device__ __forceinline__ int scr_idx<bf16_t>(int p, int c) {
-  return p * 32 + ((((c >> 2) ^ ((p >> 1) & 7))) << 2) + (c & 3);
+// 32x32 f32 scratch with a padded row stride: the CL write (fixed pixel per
+// half-wave, 32 consecutive channels) and the PA read (32 pixels, same
+// channels) are both bank-conflict free, and every address is a per-lane base
+// plus a compile-time offset (no per-register address VGPRs to hoist/spill).
+//   f32 reads  (ds_read_b32,  lane = pixel): stride 33 -> banks (p + k) % 32
+//   bf16 reads (ds_read_b128, 8 channels)  : stride 36 -> 16-B aligned rows,
+//            slot (9p + q) % 16 distinct within every 16-lane group
+template <class S> constexpr int scr_stride() { return sizeof(S) == 4 ? 33 : 36; }
+constexpr int SCR_FLOATS = 32 * 36;     // per wave
+template <class S> __device__ __forceinline__ int scr_idx(int p, int c) {
+  return p * scr_stride<S>() + c;
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -161,9 +166,8 @@ __device__ __forceinline__ void cl_to_pa(float* __restrict__ scr, const f32x16& 
   } else {
 #pragma unroll
     for (int s = 0; s < Tr<S>::KS; ++s) {
-      const int q0 = 4 * s + 2 * h;
-      const f32x4 lo = *(const f32x4*)(scr + p * 32 + ((q0 ^ ((p >> 1) & 7)) << 2));
-      const f32x4 hi = *(const f32x4*)(scr + p * 32 + (((q0 + 1) ^ ((p >> 1) & 7)) << 2));
+      const f32x4 lo = *(const f32x4*)(scr + scr_idx<S>(p, 16 * s + 8 * h));
+      const f32x4 hi = *(const f32x4*)(scr + scr_idx<S>(p, 16 * s + 8 * h + 4));
       bf16x8 f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) { f[j] = (bf16_t)lo[j]; f[4 + j] = (bf16_t)hi[j]; }
@@ -227,16 +231,28 @@ __device__ void tile_zero(S* tile, int tid) {
 }
 
 // Fill the tile interior with channels [pass*CP, pass*CP+CP) of a
-// channels-last clip image (global, [32][32][32] of S).
+// channels-last clip image (global, [32][32][32] of S).  All 16 loads of a
+// thread are issued before any LDS store so one memory round trip covers the
+// whole 64 KB image (one wave per SIMD has nothing else to hide latency with).
 template <class S>
-__device__ void tile_fill(S* __restrict__ tile, const S* __restrict__ src, int pass, int tid) {
+__device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restrict__ src,
+                                          int pass, int tid) {
   constexpr int CPB = 16 / (int)sizeof(S);          // channels per 16-B chunk
   constexpr int NCH = Tr<S>::CP / CPB;               // chunks per pixel
-  for (int idx = tid; idx < NPIX * NCH; idx += NT) {
+  constexpr int PER = NPIX * NCH / NT;               // chunks per thread (16)
+  uint4 v[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int idx = tid + k * NT;
+    const int pix = idx / NCH, q = idx % NCH;
+    v[k] = *(const uint4*)(src + pix * C + pass * Tr<S>::CP + q * CPB);
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int idx = tid + k * NT;
     const int pix = idx / NCH, q = idx % NCH;
     const int y = pix >> 5, x = pix & 31;
-    const uint4 v = *(const uint4*)(src + pix * C + pass * Tr<S>::CP + q * CPB);
-    *(uint4*)(tile + tile_off<S>(y + PADMAX, x + PADMAX, q * CPB)) = v;
+    *(uint4*)(tile + tile_off<S>(y + PADMAX, x + PADMAX, q * CPB)) = v[k];
   }
 }
 
@@ -244,12 +260,12 @@ __device__ void tile_fill(S* __restrict__ tile, const S* __restrict__ src, int p
 //   acc[i][x][n] += sum_{tap,ci} in[row0+i+kh-pad][x+kw-pad][ci] * W[n][ci][tap]
 // wf: B fragments [K*K][KS][64] (prepared by k_prep), streamed from L2 with a
 // two-tap-deep register prefetch so each tap's 16 (bf16) MFMAs never wait on
-// a global load.  The caller has zeroed the tile halo; the interior is refilled
-// per pass.
-template <class S, int K>
-__device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], const S* __restrict__ src,
+// a global load.  `fill(pass)` writes the tile interior (channels of that
+// pass); the caller has zeroed the halo.
+template <class S, int K, class Fill>
+__device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
                                            const typename Tr<S>::frag* __restrict__ wf, S* tile,
-                                           int row0, int tid, int lane) {
+                                           int row0, int lane, int ablate) {
   using TT = Tr<S>;
   using F = typename TT::frag;
   constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
@@ -258,8 +274,9 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], const S* __restri
   const int h = lane >> 5, px = lane & 31;
   for (int pass = 0; pass < TT::NPASS; ++pass) {
     __syncthreads();
-    tile_fill<S>(tile, src, pass, tid);
+    if (!(ablate & 2)) fill(pass);
     __syncthreads();
+    if (ablate & 1) continue;
     const F* w = wf + pass * KSP * 64 + lane;
     F b0[KSP], b1[KSP], b2[KSP];
 #pragma unroll
@@ -293,15 +310,15 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], const S* __restri
   }
 }
 
-template <class S>
-__device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], const S* __restrict__ src,
+template <class S, class Fill>
+__device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], Fill& fill,
                                          const typename Tr<S>::frag* __restrict__ wf, S* tile,
-                                         int K, int row0, int tid, int lane) {
+                                         int K, int row0, int lane, int ablate) {
   switch (K) {
-    case 7: conv_run_k<S, 7>(acc, src, wf, tile, row0, tid, lane); break;
-    case 5: conv_run_k<S, 5>(acc, src, wf, tile, row0, tid, lane); break;
-    case 3: conv_run_k<S, 3>(acc, src, wf, tile, row0, tid, lane); break;
-    default: conv_run_k<S, 1>(acc, src, wf, tile, row0, tid, lane); break;
+    case 7: conv_run_k<S, 7>(acc, fill, wf, tile, row0, lane, ablate); break;
+    case 5: conv_run_k<S, 5>(acc, fill, wf, tile, row0, lane, ablate); break;
+    case 3: conv_run_k<S, 3>(acc, fill, wf, tile, row0, lane, ablate); break;
+    default: conv_run_k<S, 1>(acc, fill, wf, tile, row0, lane, ablate); break;
   }
 }
 

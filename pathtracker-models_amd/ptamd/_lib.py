@@ -23,8 +23,9 @@ EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
            "pt_cell_timing_read", "pt_cell_timing_reset", "pt_last_error", "pt_version")
 
 # kernel kinds for pt_cell_timing_* (include/pt_cell.h)
-K_FWD_A, K_FWD_B, K_BWD_A, K_BWD_B, K_WGRAD, K_PREP, K_REDUCE = range(7)
-KIND_NAMES = ("k_fwd_a", "k_fwd_b", "k_bwd_a", "k_bwd_b", "k_wgrad", "k_prep", "k_reduce")
+KIND_NAMES = ("k_pw_fa", "k_conv_fa", "k_pw_fb", "k_conv_fb", "k_pw_ba", "k_conv_ba",
+              "k_pw_bb", "k_conv_bb", "k_wgrad", "k_prep", "k_reduce")
+NKINDS = len(KIND_NAMES)
 
 _P = ctypes.c_void_p
 

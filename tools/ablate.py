@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Kernel-phase ablation timing (timing experiments only; outputs are garbage
+under ablation).  PT_CELL_ABLATE bits: 1 skip conv MFMA loop, 2 skip conv tile
+fill, 4 skip per-row element-wise loops.  Masks are interleaved in one process
+(cdna_hip_programming.md §5.4 rule 24)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "pathtracker-models_amd")]
+
+import torch  # noqa: E402
+
+from ptamd import _lib  # noqa: E402
+from models import InT as int_mod  # noqa: E402
+
+
+def main():
+    b = int(os.environ.get("B", 256))
+    t = int(os.environ.get("T", 64))
+    dtype = os.environ.get("DT", "bf16")
+    masks = [int(m) for m in os.environ.get("MASKS", "0,1,2,3,4,7").split(",")]
+    rounds = int(os.environ.get("ROUNDS", 3))
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = int_mod.InT(dimensions=32, timesteps=t, kernel_size=7).to(dev)
+    m.cell_dtype = dtype
+    x = torch.rand(b, 3, t, 32, 32, device=dev)
+    lib = _lib.load()
+    kinds = list(_lib.KIND_NAMES[:9])
+    res = {mk: {k: [] for k in kinds} for mk in masks}
+    for r in range(rounds + 1):
+        for mk in masks:
+            os.environ["PT_CELL_ABLATE"] = str(mk)
+            torch.cuda.synchronize()
+            lib.pt_cell_timing_reset()
+            lib.pt_cell_timing_enable((1 << _lib.NKINDS) - 1)
+            out, _ = m(x)
+            out.sum().backward()
+            torch.cuda.synchronize()
+            lib.pt_cell_timing_enable(0)
+            if r == 0:
+                continue
+            for kind, name in enumerate(kinds):
+                ms, n = _lib.timing_read(kind)
+                if n:
+                    res[mk][name].append(1e3 * ms / n)
+    os.environ.pop("PT_CELL_ABLATE")
+    print(f"avg launch us (B={b} T={t} {dtype}), median of {rounds} rounds")
+    print("mask  " + "  ".join(f"{k[2:]:>8}" for k in kinds))
+    for mk in masks:
+        row = []
+        for k in kinds:
+            v = sorted(res[mk][k])
+            row.append(f"{v[len(v) // 2]:8.1f}" if v else " " * 8)
+        print(f"{mk:4d}  " + "  ".join(row))
+
+
+if __name__ == "__main__":
+    main()
