@@ -1,0 +1,113 @@
+"""The callers of the hot path: model registry, model step, batch preparation.
+
+Mirrors the InT half of the reference's ``utils/engine.py`` (``model_step``
+:43-74, ``model_selector`` :77-146, ``prepare_data`` :220-255) with the same
+names, arguments and return values, so a harness written against the reference
+runs unchanged.  Differences, all deliberate:
+
+* ``prepare_data`` does the uint8 -> float conversion and the
+  [B,T,H,W,3] -> [B,3,T,H,W] transpose on the device (one H2D copy of the
+  uint8 batch, 4x fewer bytes than the reference's float64 host copy).  The
+  value mapping goes through a 256-entry table built as ``float32(u / 255.)``
+  in float64, i.e. exactly the reference's numpy arithmetic, so the result is
+  bit-identical.
+* Models outside the hot path (torchvision / slowfast / transformer / kys /
+  hGRU-SEG baselines) are out of scope here and raise ``NotImplementedError``
+  with the reference's own message.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from models import InT
+
+TORCHVISION = ['r3d', 'mc3', 'r2plus1', 'nostride_r3d', 'nostride_r3d_pos']
+SLOWFAST = ['slowfast', 'slowfast_nl']
+ALL_DATASETS = [
+    {"dist": 14, "speed": 1, "length": 64},
+    {"dist": 14, "speed": 1, "length": 128},
+    {"dist": 14, "speed": 1, "length": 32},
+    {"dist": 14, "speed": 2, "length": 64},
+    {"dist": 14, "speed": 4, "length": 64},
+    {"dist": 0, "speed": 1, "length": 64},
+    {"dist": 5, "speed": 1, "length": 64},
+    {"dist": 25, "speed": 1, "length": 64},
+]
+
+# model name -> extra InT constructor arguments (utils/engine.py:77-146)
+INT_VARIANTS = {
+    'InT': {},
+    'InT_no_inh': dict(no_inh=True),
+    'InT_no_mult': dict(lesion_alpha=True, lesion_gamma=True),
+    'InT_no_add': dict(lesion_mu=True, lesion_kappa=True),
+    'InT_mult_add': dict(lesion_alpha=False, lesion_gamma=True, lesion_mu=True, lesion_kappa=False),
+    'InT_only_add': dict(lesion_alpha=True, lesion_gamma=False, lesion_mu=False, lesion_kappa=True),
+    'InT_tanh': dict(nl=F.tanh),
+}
+
+
+def _jv_one(device):
+    return torch.ones(1, dtype=torch.float32, device=device)
+
+
+def model_step(model, imgs, model_name, test=False):
+    """Pass imgs through the model (utils/engine.py:43-74)."""
+    if model_name in TORCHVISION or model_name in SLOWFAST:
+        raise NotImplementedError(f"{model_name}: feedforward baselines are outside the InT hot path")
+    if test:
+        output, states, gates = model.forward(imgs, testmode=True)
+        return output, states, gates
+    output, jv_penalty = model.forward(imgs)
+    return output, jv_penalty
+
+
+def model_selector(args, timesteps, device, fb_kernel_size=7, dimensions=32):
+    """Construct a model by name (utils/engine.py:77-146; InT variants)."""
+    extra = INT_VARIANTS.get(args.model)
+    if extra is None:
+        raise NotImplementedError("Model not found.")
+    print("Init model InT ", getattr(args, 'algo', 'bptt'), 'penalty: ', getattr(args, 'penalty', False))
+    return InT.InT(dimensions=dimensions, timesteps=timesteps, kernel_size=fb_kernel_size,
+                   jacobian_penalty=False, grad_method='bptt', **extra)
+
+
+_LUT = {}
+
+
+def _u8_to_unit(device):
+    lut = _LUT.get(device)
+    if lut is None:
+        lut = torch.from_numpy((np.arange(256, dtype=np.float64) / 255.).astype(np.float32)).to(device)
+        _LUT[device] = lut
+    return lut
+
+
+def prepare_data(imgs, target, args, device, disentangle_channels, use_augmentations=False):
+    """uint8 [B,T,H,W,3] clips + byte labels -> fp32 [B,3,T,H,W] in [0,1] + float labels.
+
+    Reference: utils/engine.py:220-255.  ``imgs`` may be a numpy array or a
+    torch tensor (host or device); ``target`` an array of 1-byte strings, of
+    uint8, or a tensor of codes.
+    """
+    if use_augmentations:
+        raise NotImplementedError("use_augmentations: the reference's transform is undefined there")
+    device = torch.device(device)
+    u8 = imgs if isinstance(imgs, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(imgs))
+    u8 = u8.to(device, non_blocking=True)
+    if not disentangle_channels:
+        x = _u8_to_unit(device)[u8.long()].permute(0, 4, 1, 2, 3).contiguous()
+    else:
+        # mask = round(sum_c u_c/255) in float64, as numpy does (:227-232)
+        v = u8.to(torch.float64) / 255.
+        mask = (v[..., 0] + v[..., 1] + v[..., 2]).round()
+        x = torch.stack([(mask == 3), (mask == 1), (mask == 2)], 1).to(torch.float32)
+    if getattr(args, 'pretrained', False):
+        mu = torch.tensor([0.43216, 0.394666, 0.37645], device=device)[None, :, None, None, None]
+        sd = torch.tensor([0.22803, 0.22145, 0.216989], device=device)[None, :, None, None, None]
+        x = (x - mu) / sd
+    if isinstance(target, torch.Tensor):
+        codes = target
+    else:
+        t = np.asarray(target)
+        codes = torch.from_numpy(np.vectorize(ord)(t) if t.dtype.kind in 'OSU' else t.astype(np.int64))
+    return x, codes.to(device, dtype=torch.float)
