@@ -15,8 +15,10 @@ N * B * K / max-over-ranks(time of K steps).  Scaling is weak (B fixed per GPU).
 
 roofline: the dominant kernel (largest summed device time inside the timed
 region, measured with HIP events the library records around its own launches
-on the launch stream) against the dense bf16 MFMA peak, with algorithmic
-FLOPs per launch from DESIGN.md §4.  cpu_baseline: the CPU oracle
+on the launch stream) against whichever roofline binds it — dense MFMA peak or
+HBM bandwidth — using the algorithmic FLOPs / bytes per launch of DESIGN.md §3;
+traffic = PMC-measured HBM bytes per launch from profiles/ (or null).
+cpu_baseline: the CPU oracle
 (oracle/cells.py, plain PyTorch fp32, the reference's own op graph) timed on
 this host for a bounded sample (rank 0, N=1 only).
 """
@@ -72,6 +74,38 @@ def algorithmic_flops(kind, batch, frames):
         "k_wgrad": frames * 2 * cf,                 # dW_inh + dW_exc
     }.get(kind, 0)
     return per_clip * batch
+
+
+def algorithmic_bytes(kind, batch, frames, elt):
+    """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
+    (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
+    XF = one clip-frame of the f32 input (3x32x32)."""
+    F, XF = C * HW * HW * elt, 3 * HW * HW * 4
+    per_clip = {
+        "k_pw_fa": frames * (XF + 7 * F),
+        "k_conv_fa": frames * 2 * F,
+        "k_pw_fb": frames * (XF + 3 * F),
+        "k_conv_fb": frames * 2 * F,
+        "k_pw_ba": frames * (XF + 12 * F),
+        "k_conv_ba": (frames - 1) * 5 * F + 3 * F,
+        "k_pw_bb": frames * (XF + 9 * F),
+        "k_conv_bb": frames * 6 * F,
+        "k_wgrad": frames * 4 * F,
+    }.get(kind, 0)
+    return per_clip * batch
+
+
+def pmc_traffic(kernel, batch, frames, dtype):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same workload), or None."""
+    import glob
+    tag = f"B={batch} T={frames} {dtype}"
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("note") == tag and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["traffic_bytes"]
+    return None
 
 
 def make_data(seed, batch, frames, device):
@@ -188,11 +222,23 @@ def main():
         value = world * args.batch * args.steps / el
         dom = max(kern, key=lambda k: kern[k][0])
         dom_ms, dom_n = kern[dom]
-        flops_step = algorithmic_flops(dom, args.batch, args.frames)
         avg_ms = dom_ms / max(dom_n, 1)
-        per_launch = flops_step * args.steps / max(dom_n, 1)
-        achieved = per_launch / (avg_ms * 1e-3) / 1e12
-        peak = PEAK_TFLOPS[args.dtype]
+        elt = 2 if args.dtype == "bf16" else 4
+        flop_launch = algorithmic_flops(dom, args.batch, args.frames) * args.steps / max(dom_n, 1)
+        byte_launch = algorithmic_bytes(dom, args.batch, args.frames, elt) * args.steps / max(dom_n, 1)
+        peak_f = PEAK_TFLOPS[args.dtype]
+        # the binding roofline: the larger of the two ideal times
+        if flop_launch / (peak_f * 1e12) >= byte_launch / (PEAK_HBM_GBS * 1e9):
+            roof = {"bound": "mfma", "achieved": round(flop_launch / (avg_ms * 1e-3) / 1e12, 2),
+                    "peak": peak_f, "unit": "TFLOP/s"}
+        else:
+            roof = {"bound": "hbm", "achieved": round(byte_launch / (avg_ms * 1e-3) / 1e9, 1),
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s"}
+        roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+        roof.update({"traffic": pmc_traffic(dom, args.batch, args.frames, args.dtype),
+                     "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
+                     "algorithmic_flop_per_launch": int(flop_launch),
+                     "algorithmic_bytes_per_launch": int(byte_launch)})
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -211,10 +257,7 @@ def main():
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "frames": args.frames, "channels": C, "kernel": K,
                        "parallelism": f"dp{world}"},
-            "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2),
-                         "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                         "traffic": None, "avg_launch_ms": round(avg_ms, 4),
-                         "launches": dom_n, "algorithmic_flop_per_launch": int(per_launch)},
+            "roofline": roof,
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
             "loss": round(float(loss.item()), 5),
         }

@@ -1,20 +1,21 @@
 // pt_cell.hip — InT recurrent cell, forward + BPTT backward, for MI355X (gfx950).
 //
 // Reference path replaced (paths relative to the reference repo):
-//   frame loop      models/InT.py:223-235          -> k_fwd_a / k_fwd_b per frame
-//   rCell.forward   models/InT.py:145-179          -> split at the two BatchNorms
-//   autograd BPTT   mainclean.py:204 (loss.backward) -> k_bwd_a / k_bwd_b per frame,
-//                                                     k_wgrad (7x7 weight grads), k_reduce
+//   stem + frame loop  models/InT.py:212-235   -> per frame: k_pw_fa, k_conv (inh),
+//                                                 k_pw_fb, k_conv (exc)
+//   rCell.forward      models/InT.py:145-179   -> split at the two BatchNorms
+//   autograd BPTT      mainclean.py:204        -> per frame: k_conv (BN1 bwd + conv^T exc),
+//                                                 k_pw_bb, k_conv (BN0 bwd + conv^T inh),
+//                                                 k_pw_ba; then k_wgrad (7x7 weight
+//                                                 grads), k_reduce
 //
-// One workgroup (4 waves) owns one clip for a whole frame step: the 32x32
-// image is exactly one 38x38 zero-halo LDS tile, so the k x k convolutions need
-// no halo exchange.  The only cross-clip coupling is BatchNorm's batch
-// statistics (track_running_stats=False, models/InT.py:102): each kernel ends
-// by publishing per-clip partial statistics, and the next kernel reduces them
-// (kernel boundary = grid-wide sync).  Per frame:
-//   FA(t): [E_{t-1} update (needs BN1(t-1))] att, gE, eg; conv(gE, w_inh) -> ci, BN0 partials
-//   FB(t): [BN0(t)] Ihat, inh gate, I_t;              conv(I_t, w_exc) -> ce, BN1 partials
-// and FA(T) closes the last frame.  Backward mirrors this (see k_bwd_a/b).
+// Conv kernels: one workgroup owns one clip; the 32x32 image is exactly one
+// 38x38 zero-halo LDS tile, so the k x k convolutions need no halo exchange.
+// Point-wise kernels: several 8-wave workgroups per clip, one or two image rows
+// per wave.  The only cross-clip coupling is BatchNorm's batch statistics
+// (track_running_stats=False, models/InT.py:102): a kernel publishes per-clip
+// partial sums (fp64 atomics), the next kernel finalises them (kernel boundary
+// = grid-wide sync).  See DESIGN.md §3.
 #include "pt_device.h"
 #include "../../include/pt_cell.h"
 
