@@ -116,36 +116,43 @@ __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps
   __syncthreads();
 }
 
-// Per-clip (mean, M2) of the conv outputs held in acc (two-pass, robust),
-// accumulated into the fp64 batch sums.
+// Per-clip (mean, M2) of the conv outputs held in acc (PL layout, two-pass,
+// robust), accumulated into the fp64 batch sums.  red: 256 floats.
 __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out, int lane,
                                int wave, int tid) {
-  float s = 0.f;
+  const int h = lane >> 5;
+  const int ch = pl_ch(pl_sum_reg(lane), h);
+  f32x16 s = acc[0];
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) s += hsum16(acc[i]);
-  s += __shfl_xor(s, 32);
-  if (lane < 32) red[wave * 32 + lane] = s;
+  for (int i = 1; i < RPW; ++i) s += acc[i];
+  const float ts = pl_lane_sum(s, lane);
+  if (!(lane & 16)) red[wave * 32 + ch] = ts;
   __syncthreads();
-  const int c = lane & 31;
-  float mean = 0.f;
+  f32x16 mean;
 #pragma unroll
-  for (int w = 0; w < NWAVE; ++w) mean += red[w * 32 + c];
-  mean *= (1.f / NPIX);
-  float m2 = 0.f;
+  for (int g = 0; g < 4; ++g) {
+    f32x4 m = *(const f32x4*)(red + 8 * g + 4 * h);
 #pragma unroll
-  for (int i = 0; i < RPW; ++i)
+    for (int w = 1; w < NWAVE; ++w) m += *(const f32x4*)(red + w * 32 + 8 * g + 4 * h);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { const float d = acc[i][r] - mean; m2 += d * d; }
-  m2 += __shfl_xor(m2, 32);
-  __syncthreads();
-  if (lane < 32) red[wave * 32 + lane] = m2;
+    for (int j = 0; j < 4; ++j) mean[4 * g + j] = m[j] * (1.f / NPIX);
+  }
+  f32x16 q = zero16();
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const f32x16 d = acc[i] - mean;
+    q += d * d;
+  }
+  const float tq = pl_lane_sum(q, lane);
+  if (!(lane & 16)) red[128 + wave * 32 + ch] = tq;
   __syncthreads();
   if (tid < 32) {
-    float v = 0.f;
+    float sm = 0.f, v = 0.f;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) v += red[w * 32 + tid];
-    unsafeAtomicAdd(out + tid, (double)mean);
-    unsafeAtomicAdd(out + 32 + tid, (double)mean * (double)mean);
+    for (int w = 0; w < NWAVE; ++w) { sm += red[w * 32 + tid]; v += red[128 + w * 32 + tid]; }
+    const double mn = (double)(sm * (1.f / NPIX));
+    unsafeAtomicAdd(out + tid, mn);
+    unsafeAtomicAdd(out + 32 + tid, mn * mn);
     unsafeAtomicAdd(out + 64 + tid, (double)v);
   }
 }
@@ -183,9 +190,9 @@ struct ConvArgs {
   const S *add0, *add1;         // EPI_ADD (add1 may be null)
 };
 
-constexpr int CONV_MISC = 512;  // floats: red[128] + bn-bwd table [3][32]
+constexpr int CONV_MISC = 512;  // floats: red[256] (bn-bwd table [3][32] aliases it)
 template <class S>
-constexpr int conv_lds_bytes() { return tile_bytes<S>() + CONV_MISC * 4; }
+constexpr int conv_lds_bytes() { return tile_bytes<S>() + CONV_MISC * 4 + 2 * WSLICE_BYTES; }
 
 template <class S, int FILL, int EPI>
 __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
@@ -193,6 +200,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
   S* tile = (S*)smem;
   float* red = (float*)(smem + tile_bytes<S>());
   float* tbl = red + 128;       // FILL_BNBWD: per-channel A, Bc, Cc
+  char* wbuf = (char*)(red + CONV_MISC);   // 2 weight slices
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
@@ -264,19 +272,21 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
     f32x16 acc[RPW];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) acc[i] = zero16();
-    conv_run<S>(acc, fill, a.wf, tile, a.K, wave * RPW, lane, a.ablate);
+    conv_run<S>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate);
+    const int px = lane & 31;
     if constexpr (EPI == EPI_FWD) {
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
-        store_cl(a.out_raw + cb + (size_t)(wave * RPW + i) * IMG * C, c, h, acc[i]);
+        store_pl(a.out_raw + cb + ((size_t)(wave * RPW + i) * IMG + px) * C, h, acc[i]);
       bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
     } else {
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
-        const size_t ro = cb + (size_t)(wave * RPW + i) * IMG * C;
-        f32x16 v = acc[i] + load_cl(a.add0 + ro, c, h);
-        if (a.add1) v += load_cl(a.add1 + ro, c, h);
-        store_cl(a.out + ro, c, h, v);
+        const size_t po = cb + ((size_t)(wave * RPW + i) * IMG + px) * C;
+        f32x16 v = acc[i];
+        add_pl(a.add0 + po, h, v);
+        if (a.add1) add_pl(a.add1 + po, h, v);
+        store_pl(a.out + po, h, v);
       }
     }
   }

@@ -39,6 +39,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16_t;
+// native 16-B vector (HIP's uint4 is a struct whose copies lower to memcpy,
+// which can pin arrays of it in scratch)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <class S> struct Tr;
 template <> struct Tr<float> {
@@ -88,6 +91,64 @@ template <class S>
 __device__ __forceinline__ void store_cl(S* __restrict__ row, int c, int h, const f32x16& v) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) stf(row + cl_x(r, h) * C + c, v[r]);
+}
+
+// PL ("pixel on lane"): the C/D layout of the transposed product D^T[n][p]
+// (conv kernels put the weights on the A side): lane l -> pixel p = l & 31,
+// half h = l >> 5; reg r -> channel pl_ch(r, h) = (r & 3) + 8 (r >> 2) + 4 h.
+// A lane's 16 channels are 4 runs of 4 contiguous channels, so a row tile
+// moves with 4 x 16 B (f32) / 4 x 8 B (bf16) accesses per lane.
+__device__ __forceinline__ int pl_ch(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// px: pointer to channel 0 of this lane's pixel in a channels-last image.
+__device__ __forceinline__ void store_pl(float* __restrict__ px, int h, const f32x16& v) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *(f32x4*)(px + 8 * g + 4 * h) = f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+}
+__device__ __forceinline__ void store_pl(bf16_t* __restrict__ px, int h, const f32x16& v) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *(bf16x4*)(px + 8 * g + 4 * h) = bf16x4{(bf16_t)v[4 * g], (bf16_t)v[4 * g + 1],
+                                            (bf16_t)v[4 * g + 2], (bf16_t)v[4 * g + 3]};
+}
+__device__ __forceinline__ void add_pl(const float* __restrict__ px, int h, f32x16& v) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 a = *(const f32x4*)(px + 8 * g + 4 * h);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * g + j] += a[j];
+  }
+}
+__device__ __forceinline__ void add_pl(const bf16_t* __restrict__ px, int h, f32x16& v) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const bf16x4 a = *(const bf16x4*)(px + 8 * g + 4 * h);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * g + j] += (float)a[j];
+  }
+}
+
+// Sum a PL tile's 16 registers over the 32 pixel lanes of each half by
+// recursive halving (16 cross-lane moves instead of 5 x 16): on return lane l
+// holds the total of register pl_sum_reg(l) (channel pl_ch(pl_sum_reg(l), h));
+// lanes l and l ^ 16 hold the same value.
+__device__ __forceinline__ int pl_sum_reg(int lane) {
+  const int q = lane & 15;
+  return 8 * (q & 1) + 4 * ((q >> 1) & 1) + 2 * ((q >> 2) & 1) + ((q >> 3) & 1);
+}
+__device__ __forceinline__ float pl_lane_sum(const f32x16& v, int lane) {
+  float a[8], b[4], c[2];
+  const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    a[j] = (b0 ? v[j + 8] : v[j]) + __shfl_xor(b0 ? v[j] : v[j + 8], 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = (b1 ? a[j + 4] : a[j]) + __shfl_xor(b1 ? a[j] : a[j + 4], 2);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) c[j] = (b2 ? b[j + 2] : b[j]) + __shfl_xor(b2 ? b[j] : b[j + 2], 4);
+  float d = (b3 ? c[1] : c[0]) + __shfl_xor(b3 ? c[0] : c[1], 8);
+  return d + __shfl_xor(d, 16);
 }
 
 __device__ __forceinline__ f32x16 zero16() {
@@ -256,56 +317,127 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
   }
 }
 
-// Implicit-GEMM k x k conv over the LDS tile for this wave's RPW rows:
-//   acc[i][x][n] += sum_{tap,ci} in[row0+i+kh-pad][x+kw-pad][ci] * W[n][ci][tap]
-// wf: B fragments [K*K][KS][64] (prepared by k_prep), streamed from L2 with a
-// two-tap-deep register prefetch so each tap's 16 (bf16) MFMAs never wait on
-// a global load.  `fill(pass)` writes the tile interior (channels of that
-// pass); the caller has zeroed the halo.
+// Implicit-GEMM k x k conv over the LDS tile for this wave's RPW rows, computed
+// transposed so the result lands in the PL layout (lane = pixel):
+//   acc[i][n][x] += sum_{tap,ci} W[n][ci][tap] * in[row0+i+kh-pad][x+kw-pad][ci]
+// Column-tap-major with row reuse: for one kernel column kw the wave walks the
+// RPW+K-1 tile rows it touches; each A fragment (tile row, kw, k-step) is read
+// from LDS ONCE and feeds the K MFMAs (kh = 0..K-1) of the output rows
+// i = tr - kh it contributes to (K x fewer A reads than tap-major order).
+// B fragments: wf is [K*K][KS][64] (prepared by k_prep).  The K taps of one
+// column (one "slice", 14 KB) are staged in LDS, double-buffered: the slice of
+// column kw+1 is fetched from L2 into registers at the top of column kw and
+// written to LDS after its MFMAs, so no MFMA ever waits on an L2 round trip
+// and each workgroup reads the weights once instead of once per wave.
+constexpr int CONV_PF = 3;          // A-fragment prefetch depth (tile rows)
+constexpr int WSLICE_CHUNKS = 896;   // 16-B chunks per slice: 7 taps x 2 x 64 x 16 B (bf16)
+                                     //                       = 7 taps x 8 x 64 x 4 B (f32, per pass)
+constexpr int WSLICE_BYTES = WSLICE_CHUNKS * 16;
+constexpr int WSLICE_PER = (WSLICE_CHUNKS + NT - 1) / NT;   // chunks per thread (4)
+
+// A slice in flight: four named chunks (an array here ends up in scratch).
+struct WSlice { u32x4 v0, v1, v2, v3; };
+template <int J> __device__ __forceinline__ u32x4& wsl(WSlice& w) {
+  if constexpr (J == 0) return w.v0;
+  else if constexpr (J == 1) return w.v1;
+  else if constexpr (J == 2) return w.v2;
+  else return w.v3;
+}
+static_assert(WSLICE_PER == 4, "WSlice holds 4 chunks per thread");
+
+template <class S, int K, int J>
+__device__ __forceinline__ void wslice_load1(WSlice& r, const typename Tr<S>::frag* __restrict__ wf,
+                                             int pass, int kw, int tid) {
+  using TT = Tr<S>;
+  constexpr int KSP = TT::KS / TT::NPASS;
+  constexpr int RC = 64 * (int)sizeof(typename TT::frag) / 16;   // chunks per (tap, k-step) row
+  constexpr int N = K * KSP * RC;
+  // unconditional (clamped) loads: predicated ones get parked in scratch
+  const int e = tid + J * NT < N ? tid + J * NT : N - 1;
+  const int kh = e / (KSP * RC), rem = e - kh * (KSP * RC);
+  const int s = rem / RC, q = rem - s * RC;
+  wsl<J>(r) = ((const u32x4*)(wf + ((kh * K + kw) * TT::KS + pass * KSP + s) * 64))[q];
+}
+template <class S, int K>
+__device__ __forceinline__ void wslice_load(WSlice& r, const typename Tr<S>::frag* __restrict__ wf,
+                                            int pass, int kw, int tid) {
+  wslice_load1<S, K, 0>(r, wf, pass, kw, tid);
+  wslice_load1<S, K, 1>(r, wf, pass, kw, tid);
+  wslice_load1<S, K, 2>(r, wf, pass, kw, tid);
+  wslice_load1<S, K, 3>(r, wf, pass, kw, tid);
+}
+template <int K>
+__device__ __forceinline__ void wslice_store(WSlice& r, char* buf, int tid) {
+  u32x4* b = (u32x4*)buf;
+  b[tid] = r.v0;
+  b[tid + NT] = r.v1;
+  b[tid + 2 * NT] = r.v2;
+  if (tid + 3 * NT < WSLICE_CHUNKS) b[tid + 3 * NT] = r.v3;
+}
+
 template <class S, int K, class Fill>
 __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
                                            const typename Tr<S>::frag* __restrict__ wf, S* tile,
-                                           int row0, int lane, int ablate) {
+                                           char* wbuf, int row0, int lane, int tid, int ablate) {
   using TT = Tr<S>;
   using F = typename TT::frag;
   constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
-  constexpr int KK = K * K;
   constexpr int off = PADMAX - K / 2;
+  constexpr int NTR = RPW + K - 1;          // tile rows touched by this wave
   const int h = lane >> 5, px = lane & 31;
   for (int pass = 0; pass < TT::NPASS; ++pass) {
+    WSlice pre;
+    wslice_load<S, K>(pre, wf, pass, 0, tid);
     __syncthreads();
     if (!(ablate & 2)) fill(pass);
+    wslice_store<K>(pre, wbuf, tid);
     __syncthreads();
     if (ablate & 1) continue;
-    const F* w = wf + pass * KSP * 64 + lane;
-    F b0[KSP], b1[KSP], b2[KSP];
+    for (int kw = 0; kw < K; ++kw) {
+      const F* wl = (const F*)(wbuf + (kw & 1) * WSLICE_BYTES) + lane;
+      if (kw + 1 < K) wslice_load<S, K>(pre, wf, pass, kw + 1, tid);
+      F bc[K][KSP];
 #pragma unroll
-    for (int s = 0; s < KSP; ++s) {
-      b0[s] = w[(0 * TT::KS + s) * 64];
-      b1[s] = w[((KK > 1 ? 1 : 0) * TT::KS + s) * 64];
-    }
-    for (int tap = 0; tap < KK; ++tap) {
-      const int tn = tap + 2 < KK ? tap + 2 : KK - 1;
+      for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-      for (int s = 0; s < KSP; ++s) b2[s] = w[(tn * TT::KS + s) * 64];
-      const int kh = tap / K, kw = tap - kh * K;
+        for (int s = 0; s < KSP; ++s) bc[kh][s] = wl[(kh * KSP + s) * 64];
       const int tcol = px + kw + off;
+      // A fragments of tile row tr, software-pipelined CONV_PF rows ahead of
+      // their MFMAs (one wave per SIMD: nothing else hides LDS latency)
+      F av[NTR][KSP];
+      auto load_a = [&](int tr) {
+        const int trow = row0 + tr + off;
 #pragma unroll
-      for (int s = 0; s < KSP; ++s) {
-#pragma unroll
-        for (int i = 0; i < RPW; ++i) {
-          const int trow = row0 + i + kh + off;
-          F a;
+        for (int s = 0; s < KSP; ++s) {
           if constexpr (sizeof(S) == 4) {
-            a = tile[tile_off<S>(trow, tcol, 2 * s + h)];
+            av[tr][s] = tile[tile_off<S>(trow, tcol, 2 * s + h)];
           } else {
-            a = *(const bf16x8*)(tile + tile_off<S>(trow, tcol, 16 * s + 8 * h));
+            av[tr][s] = *(const bf16x8*)(tile + tile_off<S>(trow, tcol, 16 * s + 8 * h));
           }
-          acc[i] = TT::mma(a, b0[s], acc[i]);
         }
-      }
+      };
+      constexpr int PF = CONV_PF < NTR ? CONV_PF : NTR;
 #pragma unroll
-      for (int s = 0; s < KSP; ++s) { b0[s] = b1[s]; b1[s] = b2[s]; }
+      for (int tr = 0; tr < PF; ++tr) load_a(tr);
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr) {
+        if (tr + PF < NTR) load_a(tr + PF);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < KSP; ++s) {
+          // D^T[n][p] += W[n][k] X^T[k][p]: weights on A, pixels on B -> PL output
+#pragma unroll
+          for (int kh = 0; kh < K; ++kh) {
+            const int i = tr - kh;
+            if (i >= 0 && i < RPW) acc[i] = TT::mma(bc[kh][s], av[tr][s], acc[i]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (kw + 1 < K) {
+        wslice_store<K>(pre, wbuf + ((kw + 1) & 1) * WSLICE_BYTES, tid);
+        __syncthreads();
+      }
     }
   }
 }
@@ -313,12 +445,13 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
 template <class S, class Fill>
 __device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], Fill& fill,
                                          const typename Tr<S>::frag* __restrict__ wf, S* tile,
-                                         int K, int row0, int lane, int ablate) {
+                                         char* wbuf, int K, int row0, int lane, int tid,
+                                         int ablate) {
   switch (K) {
-    case 7: conv_run_k<S, 7>(acc, fill, wf, tile, row0, lane, ablate); break;
-    case 5: conv_run_k<S, 5>(acc, fill, wf, tile, row0, lane, ablate); break;
-    case 3: conv_run_k<S, 3>(acc, fill, wf, tile, row0, lane, ablate); break;
-    default: conv_run_k<S, 1>(acc, fill, wf, tile, row0, lane, ablate); break;
+    case 7: conv_run_k<S, 7>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
+    case 5: conv_run_k<S, 5>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
+    case 3: conv_run_k<S, 3>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
+    default: conv_run_k<S, 1>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
   }
 }
 
