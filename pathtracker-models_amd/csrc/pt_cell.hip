@@ -87,13 +87,14 @@ __device__ void stage_x(const float* __restrict__ x, f32x4* xs, int b, int t, in
 
 // Stem (models/InT.py:212-213): z = W_pre x + b; xbn = nl(z); CL layout.
 struct Stem { float w0, w1, w2, b; };
-__device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const Stem& st, int act,
+template <int ACT>
+__device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const Stem& st,
                                         f32x16& z, f32x16& xv) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const f32x4 v = xs[yl * IMG + cl_x(r, h)];
     z[r] = st.w0 * v[0] + st.w1 * v[1] + st.w2 * v[2] + st.b;
-    xv[r] = act_f(z[r], act);
+    xv[r] = Act<ACT>::f(z[r]);
   }
 }
 
@@ -300,15 +301,17 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
 constexpr int PW_NT = 512;
 constexpr int PW_NW = PW_NT / 64;
 constexpr int PWF_RPP = 1;                         // forward rows per wave
-constexpr int PWB_RPP = 2;                         // backward rows per wave
+constexpr int PWA_RPP = 2;                         // k_pw_ba rows per wave
+constexpr int PWB_RPP = 1;                         // k_pw_bb rows per wave (register bound)
 constexpr int PWF_WGPC = IMG / (PW_NW * PWF_RPP);  // workgroups per clip (4)
-constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (2)
-constexpr int PW_PARTS = PWB_WGPC;                 // slab partitions per clip
+constexpr int PWA_WGPC = IMG / (PW_NW * PWA_RPP);  // (2)
+constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (4)
+constexpr int PW_PARTS = PWB_WGPC;                 // slab partitions per clip (>= PWA_WGPC)
 
 constexpr int PW_NGACC = 4;   // 1x1 weight-gradient tiles accumulated in LDS per workgroup
-template <int RPP>
+template <int RPP, bool BWD>
 constexpr int pw_lds_bytes() {   // forward point-wise kernels use xs, scr, stat only
-  return RPP == PWF_RPP
+  return !BWD
              ? PW_NW * RPP * IMG * 16 + PW_NW * SCR_FLOATS * 4 + 128 * 4
              : PW_NW * RPP * IMG * 16 /*xs*/ + PW_NW * SCR_FLOATS * 4 /*scr*/ + 128 * 4 /*stat*/ +
                    PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ +
@@ -340,9 +343,9 @@ __device__ __forceinline__ PLds pcarve(char* smem) {
 // one MFMA pair from CL registers) into the workgroup accumulator: every wave
 // parks its tile in its own flush slot, then each thread sums its elements
 // over the waves (plain stores, no atomics; all waves call this uniformly).
-template <class S>
+template <class S, class V>
 __device__ __forceinline__ void gacc_row(float* gacc_g, float* flush, const f32x16& d,
-                                         const f32x16& x, int lane, int wave, int tid) {
+                                         const V& x, int lane, int wave, int tid) {
   const f32x16 t = wgrad_cl<S>(d, x, zero16());
   const int ci = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -410,7 +413,7 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int 
 //           eg = sig(e_w I_{t-1} + e_u gE) (:171, uses the OLD inhibition;
 //           no_inh: e_w E_{t-1}, :168)
 // -------------------------------------------------------------------------
-template <class S>
+template <class S, int ACT>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -448,14 +451,14 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float cn = bw1 * ((cev[r] - m1) * rs1) + bb1;
-        const float eh = act_f(cn * (kap * Iv[r] + gam), a.act);
+        const float eh = Act<ACT>::f(cn * (kap * Iv[r] + gam));
         Ep[r] = (1.f - egv[r]) * Eo[r] + egv[r] * eh;
       }
       store_cl(a.E + (t - 1) * fs + ro, c, h, Ep);
     }
     if (t == T) continue;
     f32x16 z, xv;
-    stem_cl(L.xs, yl, h, st, a.act, z, xv);
+    stem_cl<ACT>(L.xs, yl, h, st, z, xv);
     F pax[Tr<S>::KS], pae[Tr<S>::KS];
     cl_to_pa<S>(wscr, xv, lane, pax);
     cl_to_pa<S>(wscr, Ep, lane, pae);
@@ -490,7 +493,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
 //   (:162), ig = sig(i_w x + i_u I) (:165), I_t = (1-ig) I + ig Ihat (:166)
 //   [no_inh: I_t = gE (:168)]
 // -------------------------------------------------------------------------
-template <class S>
+template <class S, int ACT>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_fb(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -525,11 +528,11 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fb(CellArgs<S> a) {
       const f32x16 civ = load_cl(a.ci + t * fs + ro, c, h);
       const f32x16 Iv = t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16();
       f32x16 z, xv, ih;
-      stem_cl(L.xs, yl, h, st, a.act, z, xv);
+      stem_cl<ACT>(L.xs, yl, h, st, z, xv);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float cn = bw0 * ((civ[r] - m0) * rs0) + bb0;
-        ih[r] = act_f(xv[r] - act_f(cn * (al * Iv[r] + mu), a.act), a.act);
+        ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * Iv[r] + mu)));
       }
       F pax[Tr<S>::KS], pai[Tr<S>::KS];
       cl_to_pa<S>(wscr, xv, lane, pax);
@@ -558,23 +561,23 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fb(CellArgs<S> a) {
 //     (:175, :173) -> d_eg, dc_e (-> BN1 bwd sums), kappa/gamma grads,
 //     dI_t (local), dE_{t-1} partial = (1-eg) dE_t.
 // -------------------------------------------------------------------------
-template <class S>
+template <class S, int ACT>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const PLds L = pcarve<PWB_RPP>(smem);
+  const PLds L = pcarve<PWA_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x / PWB_WGPC, part = blockIdx.x % PWB_WGPC;
+  const int b = blockIdx.x / PWA_WGPC, part = blockIdx.x % PWA_WGPC;
   const int t = a.t, T = a.T, B = a.B;
-  const int y0 = part * PW_NW * PWB_RPP;
+  const int y0 = part * PW_NW * PWA_RPP;
   float* wscr = L.scr + wave * SCR_FLOATS;
   const size_t fs = fr_off(1, B), cb = clip_off(b);
   const int tt = t + 1;
   const bool tail = tt <= T - 1, head = t >= 0;
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
-  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWB_RPP, tid, PW_NT);
+  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWA_RPP, tid, PW_NT);
   gacc_zero(L.gacc, 2, tid);
   __syncthreads();
 
@@ -590,13 +593,13 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   const S* dgsrc = a.conv_done ? a.dgE : a.dgEp;
 
 #pragma unroll 1
-  for (int i = 0; i < PWB_RPP && !(a.ablate & 4); ++i) {
-    const int yl = wave * PWB_RPP + i, y = y0 + yl;
+  for (int i = 0; i < PWA_RPP && !(a.ablate & 4); ++i) {
+    const int yl = wave * PWA_RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 GE;
     if (tail) {
       f32x16 z, xv;
-      stem_cl(L.xs, yl, h, st, a.act, z, xv);
+      stem_cl<ACT>(L.xs, yl, h, st, z, xv);
       f32x16 dx = load_cl(a.dxp + ro, c, h);
       if (head) {
         const f32x16 dgE = load_cl(dgsrc + ro, c, h);
@@ -627,7 +630,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const f32x4 xin = L.xs[yl * IMG + cl_x(r, h)];
-        const float dz = dx[r] * act_d(z[r], a.act);
+        const float dz = dx[r] * Act<ACT>::d(z[r]);
         sm[5] += dz * xin[0]; sm[6] += dz * xin[1]; sm[7] += dz * xin[2]; sm[8] += dz;
       }
     } else {
@@ -645,9 +648,10 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
         const float cn = bw1 * xe + bb1;
         const float w = kap * Iv[r] + gam;
         const float pe = cn * w;
-        const float eh = act_f(pe, a.act);
+        float eh, ehd;
+        Act<ACT>::fd(pe, eh, ehd);
         const float deg = GE[r] * (eh - Eo[r]);
-        const float dpe = GE[r] * egv[r] * act_d(pe, a.act);
+        const float dpe = GE[r] * egv[r] * ehd;
         const float dce = dpe * w;
         const float dw = dpe * cn;
         sm[1] += dw * Iv[r];
@@ -679,7 +683,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 //   dx_t partial, dI_{t-1}; exc gate backward (:171) -> e_w/e_u grads,
 //   dI_{t-1}, dgE partial.
 // -------------------------------------------------------------------------
-template <class S>
+template <class S, int ACT>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -710,75 +714,80 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   for (int i = 0; i < PWB_RPP && !(a.ablate & 4); ++i) {
     const int yl = wave * PWB_RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
-    // exc gate first (:171): eg = sig(e_w g_inh + e_u gE), g_inh = I_{t-1} (InT) / E_{t-1} (no_inh)
-    f32x16 eI;       // e_w^T d_e_pre, a dI_{t-1} (InT) or dE_{t-1} (no_inh) contribution
-    const f32x16 ginh = a.no_inh ? (t > 0 ? load_cl(a.E + (t - 1) * fs + ro, c, h) : zero16())
-                                 : (t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16());
+    // exc gate first (:171): eg = sig(e_w g_inh + e_u gE), g_inh = I_{t-1} (InT) / E_{t-1} (no_inh).
+    // Register budget: the loaded tiles that live through the inhibition part
+    // (ginh, dIt, ci) stay packed; e_w^T d_e_pre is folded into dI_{t-1} at the
+    // end from its 8-VGPR A fragments (pe) rather than kept as a 16-VGPR tile.
+    const Pk<S> ginh = t == 0 ? zero_pk<S>()
+                              : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
+    F pe[Tr<S>::KS];
     {
       const f32x16 dep = load_cl(a.dEp + ro, c, h);
-      const f32x16 gEv = load_cl(a.gE + t * fs + ro, c, h);
+      const Pk<S> gEv = load_pk(a.gE + t * fs + ro, c, h);
       gacc_row<S>(L.gacc + 2 * 1024, L.flush, dep, ginh, lane, wave, tid);
       gacc_row<S>(L.gacc + 3 * 1024, L.flush, dep, gEv, lane, wave, tid);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sm[3] += dep[r];
-      F pe[Tr<S>::KS];
       cl_to_pa<S>(wscr, dep, lane, pe);
-      eI = gemm_pa<S>(pe, a.gt[4], zero16(), lane);
       const f32x16 dIt0 = a.no_inh ? load_cl(a.dIt + ro, c, h) : zero16();
       const f32x16 dg = gemm_pa<S>(pe, a.gt[5], dIt0, lane);   // no_inh: I_t = gE_t
       store_cl(a.dgEp + ro, c, h, dg);
     }
     if (a.no_inh) {
-      f32x16 dEn = load_cl(a.dEn + ro, c, h);
-      dEn += eI;
+      const f32x16 dEn = gemm_pa<S>(pe, a.gt[4], load_cl(a.dEn + ro, c, h), lane);
       store_cl(a.dEn + ro, c, h, dEn);
       store_cl(a.dxp + ro, c, h, zero16());
       continue;
     }
-    const f32x16 Iv = ginh;
-    const f32x16 dIt = load_cl(a.dIt + ro, c, h);
-    const f32x16 civ = load_cl(a.ci + t * fs + ro, c, h);
+    const Pk<S> dIt = load_pk(a.dIt + ro, c, h);
+    const Pk<S> civ = load_pk(a.ci + t * fs + ro, c, h);
     f32x16 z, xv;
-    stem_cl(L.xs, yl, h, st, a.act, z, xv);
-    F pax[Tr<S>::KS], pai[Tr<S>::KS];
-    cl_to_pa<S>(wscr, xv, lane, pax);
-    cl_to_pa<S>(wscr, Iv, lane, pai);
+    stem_cl<ACT>(L.xs, yl, h, st, z, xv);
     f32x16 g = zero16();
-    g = gemm_pa<S>(pax, a.gf[2], g, lane);
-    g = gemm_pa<S>(pai, a.gf[3], g, lane);
+    {
+      F pax[Tr<S>::KS], pai[Tr<S>::KS];
+      cl_to_pa<S>(wscr, xv, lane, pax);
+      g = gemm_pa<S>(pax, a.gf[2], g, lane);
+      cl_to_pa<S>(wscr, ginh, lane, pai);
+      g = gemm_pa<S>(pai, a.gf[3], g, lane);
+    }
     f32x16 dIp, dip, dx;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float xi = (civ[r] - m0) * rs0;
+      const float Ir = (float)ginh[r], dIr = (float)dIt[r];
+      const float xi = ((float)civ[r] - m0) * rs0;
       const float cn = bw0 * xi + bb0;
-      const float u = al * Iv[r] + mu;
+      const float u = al * Ir + mu;
       const float p = cn * u;
-      const float q = xv[r] - act_f(p, a.act);
-      const float ih = act_f(q, a.act);
+      float fp, dfp, ih, dfq;
+      Act<ACT>::fd(p, fp, dfp);
+      const float q = xv[r] - fp;
+      Act<ACT>::fd(q, ih, dfq);
       const float ig = sigm(g[r] + bi);
-      const float dih = dIt[r] * ig;
-      dip[r] = dIt[r] * (ih - Iv[r]) * ig * (1.f - ig);
-      const float dq = dih * act_d(q, a.act);
-      const float dp = -dq * act_d(p, a.act);
+      const float dih = dIr * ig;
+      dip[r] = dIr * (ih - Ir) * ig * (1.f - ig);
+      const float dq = dih * dfq;
+      const float dp = -dq * dfp;
       const float du = dp * cn;
       const float dci = dp * u;
       stf(a.dcI + ro + cl_x(r, h) * C + c, dci);
       dx[r] = dq;
-      dIp[r] = dIt[r] * (1.f - ig) + du * al + eI[r];
-      sm[0] += du * Iv[r];
+      dIp[r] = dIr * (1.f - ig) + du * al;
+      sm[0] += du * Ir;
       sm[1] += du;
       sm[2] += dip[r];
       bs0 += dci;
       bs1 += dci * xi;
     }
     gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
-    gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, Iv, lane, wave, tid);
+    gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
     F pd[Tr<S>::KS];
     cl_to_pa<S>(wscr, dip, lane, pd);
     dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
-    dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
-    store_cl(a.GI + ro, c, h, dIp);
     store_cl(a.dxp + ro, c, h, dx);
+    dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
+    dIp = gemm_pa<S>(pe, a.gt[4], dIp, lane);
+    store_cl(a.GI + ro, c, h, dIp);
   }
   sm[4] = bs1;
   sm[5] = bs0;
@@ -1210,6 +1219,11 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
     if (e_ != hipSuccess) return fail(PT_ERR_HIP, "HIP error %s at line %ld", hipGetErrorString(e_), __LINE__); \
   } while (0)
 
+template <class K, class A>
+void launch_pw(K kern, dim3 grid, size_t lds, hipStream_t st, const A& a) {
+  hipLaunchKernelGGL(kern, grid, dim3(PW_NT), lds, st, a);
+}
+
 #define SETLDS(kern, bytes) \
   HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
 
@@ -1220,10 +1234,14 @@ int set_lds_attrs() {
   SETLDS((k_conv<S, FILL_COPY, EPI_FWD>), conv_lds_bytes<S>());
   SETLDS((k_conv<S, FILL_BNBWD, EPI_ADD>), conv_lds_bytes<S>());
   SETLDS((k_conv<S, FILL_BNBWD, EPI_NONE>), conv_lds_bytes<S>());
-  SETLDS(k_pw_fa<S>, pw_lds_bytes<PWF_RPP>());
-  SETLDS(k_pw_fb<S>, pw_lds_bytes<PWF_RPP>());
-  SETLDS(k_pw_ba<S>, pw_lds_bytes<PWB_RPP>());
-  SETLDS(k_pw_bb<S>, pw_lds_bytes<PWB_RPP>());
+  SETLDS((k_pw_fa<S, 0>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_fb<S, 0>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_ba<S, 0>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_bb<S, 0>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_fa<S, 1>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_fb<S, 1>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_ba<S, 1>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_bb<S, 1>), (pw_lds_bytes<PWB_RPP, true>()));
   SETLDS(k_wgrad<S>, wgrad_lds_bytes<S>());
   done = true;
   return 0;
@@ -1257,21 +1275,21 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   HIPCHK(hipMemsetAsync((char*)ws + p.o_bnacc, 0, (size_t)p.T * 2 * 96 * 8, st));
   timed(PT_K_PREP, st, [&] { hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa); });
   const dim3 gpf(p.B * PWF_WGPC);
-  const size_t lpf = pw_lds_bytes<PWF_RPP>(), lcv = conv_lds_bytes<S>();
+  const size_t lpf = (pw_lds_bytes<PWF_RPP, false>()), lcv = conv_lds_bytes<S>();
   const size_t fs = p.frame;
   ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
   ca.wf = a.wf_inh;
   cb.wf = a.wf_exc;
   for (int t = 0; t <= p.T; ++t) {
     a.t = t;
-    timed(PT_K_PW_FA, st, [&] { hipLaunchKernelGGL(k_pw_fa<S>, gpf, dim3(PW_NT), lpf, st, a); });
+    timed(PT_K_PW_FA, st, [&] { (a.act ? launch_pw(k_pw_fa<S, 1>, gpf, lpf, st, a) : launch_pw(k_pw_fa<S, 0>, gpf, lpf, st, a)); });
     if (t == p.T) break;
     if (!d->no_inh) {
       ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * 96;
       timed(PT_K_CONV_FA, st, [&] {
         hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, ca); });
     }
-    timed(PT_K_PW_FB, st, [&] { hipLaunchKernelGGL(k_pw_fb<S>, gpf, dim3(PW_NT), lpf, st, a); });
+    timed(PT_K_PW_FB, st, [&] { (a.act ? launch_pw(k_pw_fb<S, 1>, gpf, lpf, st, a) : launch_pw(k_pw_fb<S, 0>, gpf, lpf, st, a)); });
     cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * 96;
     timed(PT_K_CONV_FB, st, [&] {
       hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, cb); });
@@ -1295,13 +1313,14 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   HIPCHK(hipMemsetAsync((char*)ws + p.o_bnbacc, 0, (size_t)p.T * 2 * 64 * 8, st));
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B);
-  const dim3 gpb(p.B * PWB_WGPC);
-  const size_t lpb = pw_lds_bytes<PWB_RPP>(), lcv = conv_lds_bytes<S>();
+  const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
+  const size_t lpa = (pw_lds_bytes<PWA_RPP, true>()), lpb = (pw_lds_bytes<PWB_RPP, true>());
+  const size_t lcv = conv_lds_bytes<S>();
   const size_t fs = p.frame;
   const float* bst = a.bnstat;
   a.t = p.T - 1;
   a.conv_done = 0;
-  timed(PT_K_PW_BA, st, [&] { hipLaunchKernelGGL(k_pw_ba<S>, gpb, dim3(PW_NT), lpb, st, a); });
+  timed(PT_K_PW_BA, st, [&] { (a.act ? launch_pw(k_pw_ba<S, 1>, gpa, lpa, st, a) : launch_pw(k_pw_ba<S, 0>, gpa, lpa, st, a)); });
   for (int t = p.T - 1; t >= 0; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
@@ -1311,7 +1330,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
     timed(PT_K_CONV_BB, st, [&] {
       hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_ADD>), dim3(p.B), dim3(NT), lcv, st, cb); });
     a.t = t;
-    timed(PT_K_PW_BB, st, [&] { hipLaunchKernelGGL(k_pw_bb<S>, gpb, dim3(PW_NT), lpb, st, a); });
+    timed(PT_K_PW_BB, st, [&] { (a.act ? launch_pw(k_pw_bb<S, 1>, gpb, lpb, st, a) : launch_pw(k_pw_bb<S, 0>, gpb, lpb, st, a)); });
     a.conv_done = 0;
     if (!d->no_inh) {
       // dgE_t = conv^T(BN0-bwd(dcI), w_inh) + e_u^T d_e_pre ; frame 0's conv^T is dead (E_{-1}=0)
@@ -1329,7 +1348,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
       }
     }
     a.t = t - 1;
-    timed(PT_K_PW_BA, st, [&] { hipLaunchKernelGGL(k_pw_ba<S>, gpb, dim3(PW_NT), lpb, st, a); });
+    timed(PT_K_PW_BA, st, [&] { (a.act ? launch_pw(k_pw_ba<S, 1>, gpa, lpa, st, a) : launch_pw(k_pw_ba<S, 0>, gpa, lpa, st, a)); });
   }
   float* wslab = (float*)((char*)ws + p.o_wslab);
   const int conv0 = d->no_inh ? 1 : 0;

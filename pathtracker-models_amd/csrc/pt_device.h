@@ -39,6 +39,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16_t;
+typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
 // native 16-B vector (HIP's uint4 is a struct whose copies lower to memcpy,
 // which can pin arrays of it in scratch)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -91,6 +92,27 @@ template <class S>
 __device__ __forceinline__ void store_cl(S* __restrict__ row, int c, int h, const f32x16& v) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) stf(row + cl_x(r, h) * C + c, v[r]);
+}
+
+// Packed CL row tile in the storage type (bf16: 8 VGPRs instead of 16):
+// loaded tensors that stay live across a kernel's long middle part are kept
+// packed and widened at each use.
+template <class S> struct PkT;
+template <> struct PkT<float> { using type = f32x16; };
+template <> struct PkT<bf16_t> { using type = bf16x16; };
+template <class S> using Pk = typename PkT<S>::type;
+template <class S>
+__device__ __forceinline__ Pk<S> load_pk(const S* __restrict__ row, int c, int h) {
+  Pk<S> v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = row[cl_x(r, h) * C + c];
+  return v;
+}
+template <class S> __device__ __forceinline__ Pk<S> zero_pk() {
+  Pk<S> v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = (S)0.f;
+  return v;
 }
 
 // PL ("pixel on lane"): the C/D layout of the transposed product D^T[n][p]
@@ -184,15 +206,41 @@ __device__ __forceinline__ float ftanh(float x) {
   const float t = 1.f - 2.f * frcp(fexp(2.f * fabsf(x)) + 1.f);
   return copysignf(t, x);
 }
-__device__ __forceinline__ float act_f(float x, int act) {
-  if (act == 0) return x > 20.f ? x : __logf(1.f + fexp(x));
-  return ftanh(x);
-}
-__device__ __forceinline__ float act_d(float x, int act) {   // d nl / d x
-  if (act == 0) return x > 20.f ? 1.f : sigm(x);
-  const float t = ftanh(x);
-  return 1.f - t * t;
-}
+// Compile-time activation (a runtime switch made the compiler branch around
+// every transcendental).  Branch-free: both sides are computed and selected.
+//   softplus: f = x > 20 ? x : log(1 + e^x);  f' = x > 20 ? 1 : e^x / (1 + e^x)
+//   tanh    : f = tanh x;                     f' = 1 - tanh^2 x
+template <int ACT> struct Act;
+template <> struct Act<0> {
+  __device__ static __forceinline__ float f(float x) {
+    const float r = __logf(1.f + fexp(fminf(x, 20.f)));
+    return x > 20.f ? x : r;
+  }
+  __device__ static __forceinline__ float d(float x) {
+    const float e = fexp(fminf(x, 20.f));
+    const float r = e * frcp(1.f + e);
+    return x > 20.f ? 1.f : r;
+  }
+  // f and f' from one exponential
+  __device__ static __forceinline__ void fd(float x, float& f, float& d) {
+    const float e = fexp(fminf(x, 20.f));
+    const float s = 1.f + e;
+    const float lf = __logf(s), ld = e * frcp(s);
+    f = x > 20.f ? x : lf;
+    d = x > 20.f ? 1.f : ld;
+  }
+};
+template <> struct Act<1> {
+  __device__ static __forceinline__ float f(float x) { return ftanh(x); }
+  __device__ static __forceinline__ float d(float x) {
+    const float t = ftanh(x);
+    return 1.f - t * t;
+  }
+  __device__ static __forceinline__ void fd(float x, float& f, float& d) {
+    f = ftanh(x);
+    d = 1.f - f * f;
+  }
+};
 
 // --------------------------------------------------------- per-wave transpose
 // 32x32 f32 scratch with a padded row stride: the CL write (fixed pixel per
@@ -214,12 +262,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <class S>
-__device__ __forceinline__ void cl_to_pa(float* __restrict__ scr, const f32x16& v, int lane,
+template <class S, class V>
+__device__ __forceinline__ void cl_to_pa(float* __restrict__ scr, const V& v, int lane,
                                          typename Tr<S>::frag (&pa)[Tr<S>::KS]) {
   const int c = lane & 31, h = lane >> 5, p = lane & 31;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) scr[scr_idx<S>(cl_x(r, h), c)] = v[r];
+  for (int r = 0; r < 16; ++r) scr[scr_idx<S>(cl_x(r, h), c)] = (float)v[r];
   wave_sync();
   if constexpr (sizeof(S) == 4) {
 #pragma unroll
@@ -251,11 +299,11 @@ __device__ __forceinline__ f32x16 gemm_pa(const typename Tr<S>::frag (&pa)[Tr<S>
 // dW[n][ci] += sum_p D[p][n] X[p][ci] with D, X both in CL registers: the
 // accumulator tiles are used directly as A (= D^T) and B operands; the k
 // (pixel) order is the same permutation on both sides.
-template <class S>
-__device__ __forceinline__ f32x16 wgrad_cl(const f32x16& d, const f32x16& x, f32x16 acc) {
+template <class S, class V>
+__device__ __forceinline__ f32x16 wgrad_cl(const f32x16& d, const V& x, f32x16 acc) {
   if constexpr (sizeof(S) == 4) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = Tr<float>::mma(d[s], x[s], acc);
+    for (int s = 0; s < 16; ++s) acc = Tr<float>::mma(d[s], (float)x[s], acc);
   } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
