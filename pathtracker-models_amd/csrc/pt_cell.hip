@@ -799,13 +799,14 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   gacc_flush(L.gacc + 2 * 1024, slab_p, 4, 2, tid);
 }
 
-constexpr int WG_RB = 8;               // D rows per band
-constexpr int WG_XR = WG_RB + 2 * PADMAX;
+// D rows per band: 8 (bf16) / 4 (f32, so that two band buffers fit in LDS)
+template <class S> constexpr int wg_rb() { return sizeof(S) == 2 ? 8 : 4; }
+template <class S> constexpr int wg_xr() { return wg_rb<S>() + 2 * PADMAX; }
 constexpr int WG_NACC = 13;            // taps per wave: wave + 4 m, m < 13
 template <class S>
-constexpr int wgrad_lds_bytes() {
-  return (WG_XR * TILE * C + WG_RB * IMG * C) * (int)sizeof(S);
-}
+constexpr int wgrad_band_elems() { return wg_xr<S>() * TILE * C + wg_rb<S>() * IMG * C; }
+template <class S>
+constexpr int wgrad_lds_bytes() { return 2 * wgrad_band_elems<S>() * (int)sizeof(S); }  // 2 buffers
 
 // Unswizzled channels-last band images: the transposed 4x16 block reads
 // (ds_read_b64_tr_b16) and the f32 row reads are bank-conflict free on them,
@@ -817,15 +818,119 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 __device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
 }
+__device__ __forceinline__ bf16x8 tr_read8(const bf16_t* p) {
+  return __builtin_shufflevector(tr_read(p), tr_read(p + 4 * C), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// One band = (frame, clip, 8 D rows): the X rows y0-3 .. y0+10 (interior
+// columns; the 3 halo columns each side stay zero from the initial clear,
+// rows outside the image are written as zeros) and the 8 D rows.
+template <class S>
+struct WBand {
+  static constexpr int CPB = 16 / (int)sizeof(S);
+  static constexpr int NCH = C / CPB;
+  static constexpr int XPER = wg_xr<S>() * IMG * NCH / NT;     // 7 (bf16) / 14 (f32)
+  static constexpr int DPER = wg_rb<S>() * IMG * NCH / NT;     // 4 / 8
+  u32x4 x[XPER], d[DPER];
+  int xvalid;                                              // bit j: X chunk j inside the image
+
+  __device__ __forceinline__ void load(const S* __restrict__ Xs, const S* __restrict__ Ds, int B,
+                                       int f, int y0, int tid) {
+    const int t = f / B, b = f - t * B;
+    const S* xsrc = Xs + ((size_t)t * B + b) * NPIX * C;
+    const S* dsrc = Ds + ((size_t)t * B + b) * NPIX * C;
+    xvalid = 0;
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % NCH, pc = idx / NCH;
+      const int col = pc % IMG, row = pc / IMG;
+      const int iy = y0 + row - PADMAX;
+      const bool ok = iy >= 0 && iy < IMG;
+      const int cy = ok ? iy : 0;
+      x[j] = *(const u32x4*)(xsrc + (cy * IMG + col) * C + q * CPB);
+      xvalid |= ok << j;
+    }
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % NCH, pc = idx / NCH;
+      d[j] = *(const u32x4*)(dsrc + (y0 * IMG + pc) * C + q * CPB);
+    }
+  }
+  __device__ __forceinline__ void store(S* xt, S* dt, int tid) const {
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % NCH, pc = idx / NCH;
+      const int col = pc % IMG, row = pc / IMG;
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      *(u32x4*)(xt + wx_off(row, col + PADMAX, q * CPB)) = (xvalid >> j) & 1 ? x[j] : z;
+    }
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % NCH, pc = idx / NCH;
+      *(u32x4*)(dt + pc * C + q * CPB) = d[j];
+    }
+  }
+};
+
+// MFMAs of one band (this wave's taps {wave + 4m}).
+template <class S, int K>
+__device__ __forceinline__ void wgrad_band(f32x16 (&acc)[WG_NACC], const S* xt, const S* dt,
+                                           const int (&toff)[WG_NACC], int lane) {
+  constexpr int off = PADMAX - K / 2;
+  if constexpr (sizeof(S) == 4) {
+    // k-step = 2 pixels (x0 + h); lane&31 is ci for A, n for B
+    const int ch = lane & 31, h = lane >> 5;
+    for (int yd = 0; yd < wg_rb<S>(); ++yd) {
+      const int xb = wx_off(yd + off, h + off, ch), db = wd_off(yd, h, ch);
+      for (int x0 = 0; x0 < IMG; x0 += 2) {
+        const float bv = dt[db + x0 * C];
+#pragma unroll
+        for (int m = 0; m < WG_NACC; ++m) acc[m] = Tr<float>::mma(xt[xb + x0 * C + toff[m]], bv, acc[m]);
+      }
+    }
+  } else {
+    // k-step = 16 pixels.  Lane 4q+p' of each 16-lane group addresses pixel
+    // (x0 + 8 hh + q [+4]) and channels 16 (grp&1) + 4p' .. +3.  The 13 A
+    // fragments of the next k-step are read while this step's MFMAs run.
+    const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
+    const int chb = 16 * (grp & 1) + 4 * pp;
+    const int hh = grp >> 1;
+    constexpr int NSTEP = wg_rb<S>() * (IMG / 16);
+    auto xaddr = [&](int st) {
+      const int yd = st >> 1, dc0 = (st & 1) * 16 + 8 * hh + q;
+      return (const bf16_t*)xt + wx_off(yd + off, dc0 + off, chb);
+    };
+    auto daddr = [&](int st) {
+      const int yd = st >> 1, dc0 = (st & 1) * 16 + 8 * hh + q;
+      return (const bf16_t*)dt + wd_off(yd, dc0, chb);
+    };
+    bf16x8 av[2][WG_NACC], bv[2];
+    bv[0] = tr_read8(daddr(0));
+#pragma unroll
+    for (int m = 0; m < WG_NACC; ++m) av[0][m] = tr_read8(xaddr(0) + toff[m]);
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      const int cur = st & 1, nxt = cur ^ 1;
+      if (st + 1 < NSTEP) {
+        bv[nxt] = tr_read8(daddr(st + 1));
+#pragma unroll
+        for (int m = 0; m < WG_NACC; ++m) av[nxt][m] = tr_read8(xaddr(st + 1) + toff[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < WG_NACC; ++m) acc[m] = Tr<bf16_t>::mma(av[cur][m], bv[cur], acc[m]);
+    }
+  }
+}
 
 template <class S, int K>
 __device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __restrict__ Xs,
                                           const S* __restrict__ Ds, int B, int T, int g, int nwg,
-                                          S* xt, S* dt, int tid, int lane, int wave, int ablate) {
+                                          S* buf, int tid, int lane, int wave, int ablate) {
   constexpr int KK = K * K;
-  constexpr int off = PADMAX - K / 2;
-  constexpr int CPB = 16 / (int)sizeof(S);
-  constexpr int NCH = C / CPB;
   // wave-uniform element offset of each tap; taps beyond K*K (the 13th slot of
   // waves 1-3 at K=7) read tap 0 and their accumulator is never stored, so
   // every MFMA is unconditional (no accumulator copies around branches)
@@ -836,65 +941,31 @@ __device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __res
     const int kh = tap / K, kw = tap - kh * K;
     toff[m] = (kh * TILE + kw) * C;
   }
-  for (int f = g; f < B * T; f += nwg) {
-    const int t = f / B, b = f % B;
-    const S* xsrc = Xs + ((size_t)t * B + b) * NPIX * C;
-    const S* dsrc = Ds + ((size_t)t * B + b) * NPIX * C;
-    for (int y0 = 0; y0 < IMG; y0 += WG_RB) {
+  constexpr int BE = wgrad_band_elems<S>();
+  constexpr int NB = IMG / wg_rb<S>();                          // bands per (frame, clip)
+  const int npairs = (B * T - g + nwg - 1) / nwg;
+  const int nunits = npairs * NB;
+  // clear both buffers once (the X halo columns stay zero)
+  for (int i = tid; i < 2 * BE * (int)sizeof(S) / 16; i += NT)
+    ((u32x4*)buf)[i] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  WBand<S> band;
+  if (nunits > 0) {
+    band.load(Xs, Ds, B, g, 0, tid);
+    band.store(buf, buf + wg_xr<S>() * TILE * C, tid);
+  }
+  __syncthreads();
+  for (int u = 0; u < nunits; ++u) {
+    S* xt = buf + (u & 1) * BE;
+    S* dt = xt + wg_xr<S>() * TILE * C;
+    const bool more = u + 1 < nunits;
+    if (more && !(ablate & 128))
+      band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * wg_rb<S>(), tid);
+    if (!(ablate & 64)) wgrad_band<S, K>(acc, xt, dt, toff, lane);
+    if (more) {
+      S* xn = buf + ((u + 1) & 1) * BE;
+      if (!(ablate & 128)) band.store(xn, xn + wg_xr<S>() * TILE * C, tid);
       __syncthreads();
-      // X band: image rows y0-3 .. y0+RB+2, padded columns, zero outside
-      for (int idx = tid; idx < WG_XR * TILE * NCH && !(ablate & 128); idx += NT) {
-        const int q = idx % NCH, pc = idx / NCH;
-        const int col = pc % TILE, row = pc / TILE;
-        const int iy = y0 + row - PADMAX, ix = col - PADMAX;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (iy >= 0 && iy < IMG && ix >= 0 && ix < IMG)
-          v = *(const uint4*)(xsrc + (iy * IMG + ix) * C + q * CPB);
-        *(uint4*)(xt + wx_off(row, col, q * CPB)) = v;
-      }
-      for (int idx = tid; idx < WG_RB * IMG * NCH && !(ablate & 128); idx += NT) {
-        const int q = idx % NCH, pc = idx / NCH;
-        *(uint4*)(dt + pc * C + q * CPB) = *(const uint4*)(dsrc + (y0 * IMG + pc) * C + q * CPB);
-      }
-      __syncthreads();
-      if (ablate & 64) continue;
-      if constexpr (sizeof(S) == 4) {
-        // k-step = 2 pixels (x0 + h); lane&31 is ci for A, n for B
-        const int ch = lane & 31, h = lane >> 5;
-        for (int yd = 0; yd < WG_RB; ++yd) {
-          const int xb = wx_off(yd + off, h + off, ch), db = wd_off(yd, h, ch);
-          for (int x0 = 0; x0 < IMG; x0 += 2) {
-            const float bv = dt[db + x0 * C];
-#pragma unroll
-            for (int m = 0; m < WG_NACC; ++m) {
-              const float av = xt[xb + x0 * C + toff[m]];
-              acc[m] = Tr<float>::mma(av, bv, acc[m]);
-            }
-          }
-        }
-      } else {
-        // k-step = 16 pixels.  Lane 4q+p' of each 16-lane group addresses pixel
-        // (x0 + 8 hh + q [+4]) and channels 16 (grp&1) + 4p' .. +3.
-        const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
-        const int chb = 16 * (grp & 1) + 4 * pp;
-        const int hh = grp >> 1;
-        for (int yd = 0; yd < WG_RB; ++yd) {
-          for (int x0 = 0; x0 < IMG; x0 += 16) {
-            const int dc0 = x0 + 8 * hh + q;
-            const bf16_t* dp = (const bf16_t*)dt + wd_off(yd, dc0, chb);
-            const bf16x8 bv = __builtin_shufflevector(tr_read(dp), tr_read(dp + 4 * C),
-                                                      0, 1, 2, 3, 4, 5, 6, 7);
-            const bf16_t* xp = (const bf16_t*)xt + wx_off(yd + off, dc0 + off, chb);
-#pragma unroll
-            for (int m = 0; m < WG_NACC; ++m) {
-              const bf16_t* ap = xp + toff[m];
-              const bf16x8 av = __builtin_shufflevector(tr_read(ap), tr_read(ap + 4 * C),
-                                                        0, 1, 2, 3, 4, 5, 6, 7);
-              acc[m] = Tr<bf16_t>::mma(av, bv, acc[m]);
-            }
-          }
-        }
-      }
     }
   }
 }
@@ -909,8 +980,7 @@ __device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __res
 template <class S>
 __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, int nwg, int conv0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  S* xt = (S*)smem;
-  S* dt = xt + WG_XR * TILE * C;
+  S* buf = (S*)smem;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = blockIdx.x, conv = blockIdx.y + conv0;
@@ -922,10 +992,10 @@ __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, in
 #pragma unroll
   for (int m = 0; m < WG_NACC; ++m) acc[m] = zero16();
   switch (a.K) {
-    case 7: wgrad_run<S, 7>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
-    case 5: wgrad_run<S, 5>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
-    case 3: wgrad_run<S, 3>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
-    default: wgrad_run<S, 1>(acc, Xs, Ds, a.B, a.T, g, nwg, xt, dt, tid, lane, wave, a.ablate); break;
+    case 7: wgrad_run<S, 7>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
+    case 5: wgrad_run<S, 5>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
+    case 3: wgrad_run<S, 3>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
+    default: wgrad_run<S, 1>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
   }
   // acc[m]: rows ci = cl_x(r,h), cols n = lane&31
   float* dst = wslab + ((size_t)conv * nwg + g) * MAXTAP * 1024;
