@@ -13,9 +13,9 @@ N>1 is launched by torch.distributed.run (one rank per GPU, RCCL); rank 0
 prints ONE JSON line.  value = clips/s of the whole job (all ranks) =
 N * B * K / max-over-ranks(time of K steps).  Scaling is weak (B fixed per GPU).
 
-roofline: the dominant kernel (largest summed device time inside the timed
-region, measured with HIP events the library records around its own launches
-on the launch stream) against whichever roofline binds it — dense MFMA peak or
+roofline: the dominant kernel (largest summed device time over K further,
+instrumented steps, measured with HIP events the library records around its
+own launches on the launch stream) against whichever roofline binds it — dense MFMA peak or
 HBM bandwidth — using the algorithmic FLOPs / bytes per launch of DESIGN.md §3;
 traffic = PMC-measured HBM bytes per launch from profiles/ (or null).
 cpu_baseline: the CPU oracle
@@ -195,8 +195,8 @@ def main():
         step()
     torch.cuda.synchronize()
     lib = _lib.load()
-    lib.pt_cell_timing_reset()
-    lib.pt_cell_timing_enable((1 << _lib.NKINDS) - 1)
+    # timed region: no instrumentation (the per-launch HIP events of the
+    # kernel-timing pass below add ~1 us of stream work per launch)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -207,6 +207,12 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # kernel-timing pass (same steps, HIP events around every library launch)
+    lib.pt_cell_timing_reset()
+    lib.pt_cell_timing_enable((1 << _lib.NKINDS) - 1)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
     lib.pt_cell_timing_enable(0)
     kern = {}
     for kind, name in enumerate(_lib.KIND_NAMES):

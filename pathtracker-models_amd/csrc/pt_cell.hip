@@ -414,7 +414,8 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int 
 //           no_inh: e_w E_{t-1}, :168)
 // -------------------------------------------------------------------------
 template <class S, int ACT>
-__global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
+__global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
+  static_assert(PWF_RPP == 1, "forward point-wise kernels: one row per wave");
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const PLds L = pcarve<PWF_RPP>(smem);
@@ -422,11 +423,20 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
   const int t = a.t, T = a.T, B = a.B;
-  const int y0 = part * PW_NW * PWF_RPP;
+  const int y0 = part * PW_NW;
+  const int yl = wave, y = y0 + yl;
   float* wscr = L.scr + wave * SCR_FLOATS;
-  const size_t fs = fr_off(1, B), cb = clip_off(b);
+  const size_t fs = fr_off(1, B), ro = clip_off(b) + (size_t)y * IMG * C;
 
-  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW * PWF_RPP, tid, PW_NT);
+  // this wave's row tiles first: their latency overlaps the staging below
+  Pk<S> Iv = zero_pk<S>(), Eo = zero_pk<S>(), egv = zero_pk<S>(), cev = zero_pk<S>();
+  if (t > 0) {
+    Iv = load_pk(a.I + (t - 1) * fs + ro, c, h);
+    if (t >= 2) Eo = load_pk(a.E + (t - 2) * fs + ro, c, h);
+    egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
+    cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
+  }
+  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
   if (t > 0)
     bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * 96, B, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
@@ -438,54 +448,48 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
   const float m1 = L.stat[64 + c], rs1 = L.stat[96 + c];
   const float ba = a.gb[0][c] + a.gb[1][c], be = a.gb[4][c] + a.gb[5][c];
 
-#pragma unroll 1
-  for (int i = 0; i < PWF_RPP; ++i) {
-    const int yl = wave * PWF_RPP + i, y = y0 + yl;
-    const size_t ro = cb + (size_t)y * IMG * C;
-    f32x16 Ep = zero16(), Iv = zero16();
-    if (t > 0) {
-      Iv = load_cl(a.I + (t - 1) * fs + ro, c, h);
-      const f32x16 Eo = t >= 2 ? load_cl(a.E + (t - 2) * fs + ro, c, h) : zero16();
-      const f32x16 egv = load_cl(a.eg + (t - 1) * fs + ro, c, h);
-      const f32x16 cev = load_cl(a.ce + (t - 1) * fs + ro, c, h);
+  // close frame t-1 (:172-175)
+  f32x16 Ep = zero16();
+  if (t > 0) {
+    const float A1 = bw1 * rs1, B1 = bb1 - bw1 * rs1 * m1;     // BN1 affine folded
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float cn = bw1 * ((cev[r] - m1) * rs1) + bb1;
-        const float eh = Act<ACT>::f(cn * (kap * Iv[r] + gam));
-        Ep[r] = (1.f - egv[r]) * Eo[r] + egv[r] * eh;
-      }
-      store_cl(a.E + (t - 1) * fs + ro, c, h, Ep);
+    for (int r = 0; r < 16; ++r) {
+      const float cn = A1 * (float)cev[r] + B1;
+      const float eh = Act<ACT>::f(cn * (kap * (float)Iv[r] + gam));
+      const float e = (float)egv[r];
+      Ep[r] = (1.f - e) * (float)Eo[r] + e * eh;
     }
-    if (t == T) continue;
-    f32x16 z, xv;
-    stem_cl<ACT>(L.xs, yl, h, st, z, xv);
-    F pax[Tr<S>::KS], pae[Tr<S>::KS];
-    cl_to_pa<S>(wscr, xv, lane, pax);
-    cl_to_pa<S>(wscr, Ep, lane, pae);
-    f32x16 acc = zero16();
-    acc = gemm_pa<S>(pax, a.gf[0], acc, lane);
-    acc = gemm_pa<S>(pae, a.gf[1], acc, lane);
-    f32x16 att, gEv;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { att[r] = sigm(acc[r] + ba); gEv[r] = att[r] * Ep[r]; }
-    store_cl(a.gE + t * fs + ro, c, h, gEv);
-    if (a.gates) {
-      float* gp = a.gates + (((size_t)b * T + t) * C + c) * NPIX + y * IMG;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) gp[cl_x(r, h)] = att[r];
-    }
-    const f32x16 ginh = a.no_inh ? Ep : Iv;
-    F pag[Tr<S>::KS], pai[Tr<S>::KS];
-    cl_to_pa<S>(wscr, gEv, lane, pag);
-    cl_to_pa<S>(wscr, ginh, lane, pai);
-    acc = zero16();
-    acc = gemm_pa<S>(pai, a.gf[4], acc, lane);
-    acc = gemm_pa<S>(pag, a.gf[5], acc, lane);
-    f32x16 egn;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) egn[r] = sigm(acc[r] + be);
-    store_cl(a.eg + t * fs + ro, c, h, egn);
+    store_cl(a.E + (t - 1) * fs + ro, c, h, Ep);
   }
+  if (t == T) return;
+  f32x16 z, xv;
+  stem_cl<ACT>(L.xs, yl, h, st, z, xv);
+  F pax[Tr<S>::KS], pae[Tr<S>::KS];
+  cl_to_pa<S>(wscr, xv, lane, pax);
+  cl_to_pa<S>(wscr, Ep, lane, pae);
+  f32x16 acc = zero16();
+  acc = gemm_pa<S>(pax, a.gf[0], acc, lane);
+  acc = gemm_pa<S>(pae, a.gf[1], acc, lane);
+  f32x16 att, gEv;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { att[r] = sigm(acc[r] + ba); gEv[r] = att[r] * Ep[r]; }
+  store_cl(a.gE + t * fs + ro, c, h, gEv);
+  if (a.gates) {
+    float* gp = a.gates + (((size_t)b * T + t) * C + c) * NPIX + y * IMG;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gp[cl_x(r, h)] = att[r];
+  }
+  F pag[Tr<S>::KS], pai[Tr<S>::KS];
+  cl_to_pa<S>(wscr, gEv, lane, pag);
+  if (a.no_inh) cl_to_pa<S>(wscr, Ep, lane, pai);
+  else cl_to_pa<S>(wscr, Iv, lane, pai);
+  acc = zero16();
+  acc = gemm_pa<S>(pai, a.gf[4], acc, lane);
+  acc = gemm_pa<S>(pag, a.gf[5], acc, lane);
+  f32x16 egn;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) egn[r] = sigm(acc[r] + be);
+  store_cl(a.eg + t * fs + ro, c, h, egn);
 }
 
 // -------------------------------------------------------------------------
@@ -494,7 +498,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fa(CellArgs<S> a) {
 //   [no_inh: I_t = gE (:168)]
 // -------------------------------------------------------------------------
 template <class S, int ACT>
-__global__ __launch_bounds__(PW_NT, 2) void k_pw_fb(CellArgs<S> a) {
+__global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const PLds L = pcarve<PWF_RPP>(smem);
@@ -502,54 +506,55 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_fb(CellArgs<S> a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
   const int t = a.t, T = a.T, B = a.B;
-  const int y0 = part * PW_NW * PWF_RPP;
+  const int y0 = part * PW_NW;
+  const int yl = wave, y = y0 + yl;
   float* wscr = L.scr + wave * SCR_FLOATS;
-  const size_t fs = fr_off(1, B), cb = clip_off(b);
+  const size_t fs = fr_off(1, B), ro = clip_off(b) + (size_t)y * IMG * C;
 
-  if (!a.no_inh) {
-    stage_x(a.x, L.xs, b, t, T, y0, PW_NW * PWF_RPP, tid, PW_NT);
-    bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * 96, B, a.eps, L.stat,
-                    blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
+  if (a.no_inh) {      // I_t = gE_t (:168)
+    if (!(a.ablate & 4)) {
+      const Pk<S> g = load_pk(a.gE + t * fs + ro, c, h);
+      f32x16 v;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = (float)g[r];
+      store_cl(a.I + t * fs + ro, c, h, v);
+    }
+    return;
   }
+  const Pk<S> civ = load_pk(a.ci + t * fs + ro, c, h);
+  const Pk<S> Iv = t > 0 ? load_pk(a.I + (t - 1) * fs + ro, c, h) : zero_pk<S>();
+  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
+  bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * 96, B, a.eps, L.stat,
+                  blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
   const float m0 = L.stat[c], rs0 = L.stat[32 + c];
+  const float A0 = bw0 * rs0, B0 = bb0 - bw0 * rs0 * m0;     // BN0 affine folded
   const float bi = a.gb[2][c] + a.gb[3][c];
 
-#pragma unroll 1
-  for (int i = 0; i < PWF_RPP; ++i) {
-    const int yl = wave * PWF_RPP + i, y = y0 + yl;
-    const size_t ro = cb + (size_t)y * IMG * C;
-    f32x16 In;
-    if (!a.no_inh) {
-      const f32x16 civ = load_cl(a.ci + t * fs + ro, c, h);
-      const f32x16 Iv = t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16();
-      f32x16 z, xv, ih;
-      stem_cl<ACT>(L.xs, yl, h, st, z, xv);
+  f32x16 z, xv, ih;
+  stem_cl<ACT>(L.xs, yl, h, st, z, xv);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float cn = bw0 * ((civ[r] - m0) * rs0) + bb0;
-        ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * Iv[r] + mu)));
-      }
-      F pax[Tr<S>::KS], pai[Tr<S>::KS];
-      cl_to_pa<S>(wscr, xv, lane, pax);
-      cl_to_pa<S>(wscr, Iv, lane, pai);
-      f32x16 acc = zero16();
-      acc = gemm_pa<S>(pax, a.gf[2], acc, lane);
-      acc = gemm_pa<S>(pai, a.gf[3], acc, lane);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float ig = sigm(acc[r] + bi);
-        In[r] = (1.f - ig) * Iv[r] + ig * ih[r];
-      }
-    } else {
-      In = load_cl(a.gE + t * fs + ro, c, h);
-    }
-    store_cl(a.I + t * fs + ro, c, h, In);
+  for (int r = 0; r < 16; ++r) {
+    const float cn = A0 * (float)civ[r] + B0;
+    ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * (float)Iv[r] + mu)));
   }
+  F pax[Tr<S>::KS], pai[Tr<S>::KS];
+  cl_to_pa<S>(wscr, xv, lane, pax);
+  cl_to_pa<S>(wscr, Iv, lane, pai);
+  f32x16 acc = zero16();
+  acc = gemm_pa<S>(pax, a.gf[2], acc, lane);
+  acc = gemm_pa<S>(pai, a.gf[3], acc, lane);
+  f32x16 In;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float ig = sigm(acc[r] + bi);
+    In[r] = (1.f - ig) * (float)Iv[r] + ig * ih[r];
+  }
+  store_cl(a.I + t * fs + ro, c, h, In);
 }
 
 // -------------------------------------------------------------------------
@@ -685,6 +690,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 // -------------------------------------------------------------------------
 template <class S, int ACT>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
+  static_assert(PWB_RPP == 1, "k_pw_bb: one row per wave");
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const PLds L = pcarve<PWB_RPP>(smem);
@@ -692,12 +698,26 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x / PWB_WGPC, part = blockIdx.x % PWB_WGPC;
   const int t = a.t, T = a.T, B = a.B;
-  const int y0 = part * PW_NW * PWB_RPP;
+  const int y0 = part * PW_NW;
+  const int yl = wave, y = y0 + yl;
   float* wscr = L.scr + wave * SCR_FLOATS;
-  const size_t fs = fr_off(1, B), cb = clip_off(b);
+  const size_t fs = fr_off(1, B), ro = clip_off(b) + (size_t)y * IMG * C;
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
-  stage_x(a.x, L.xs, b, t, T, y0, PW_NW * PWB_RPP, tid, PW_NT);
+  // row tiles first (their latency overlaps the staging): g_inh = I_{t-1}
+  // (InT) / E_{t-1} (no_inh) and gE_t feed the exc gate (:171), dI_t and c_i
+  // the inhibition backward.  Kept packed; e_w^T d_e_pre is folded into
+  // dI_{t-1} at the end from its A fragments (pe) rather than kept as a tile.
+  const Pk<S> ginh = t == 0 ? zero_pk<S>()
+                            : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
+  const Pk<S> dep = load_pk(a.dEp + ro, c, h);
+  const Pk<S> gEv = load_pk(a.gE + t * fs + ro, c, h);
+  Pk<S> dIt = zero_pk<S>(), civ = zero_pk<S>();
+  if (!a.no_inh) {
+    dIt = load_pk(a.dIt + ro, c, h);
+    civ = load_pk(a.ci + t * fs + ro, c, h);
+  }
+  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
   gacc_zero(L.gacc, 4, tid);
   __syncthreads();
 
@@ -710,25 +730,16 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   const int slots[6] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B};
   float bs0 = 0.f, bs1 = 0.f;
 
-#pragma unroll 1
-  for (int i = 0; i < PWB_RPP && !(a.ablate & 4); ++i) {
-    const int yl = wave * PWB_RPP + i, y = y0 + yl;
-    const size_t ro = cb + (size_t)y * IMG * C;
-    // exc gate first (:171): eg = sig(e_w g_inh + e_u gE), g_inh = I_{t-1} (InT) / E_{t-1} (no_inh).
-    // Register budget: the loaded tiles that live through the inhibition part
-    // (ginh, dIt, ci) stay packed; e_w^T d_e_pre is folded into dI_{t-1} at the
-    // end from its 8-VGPR A fragments (pe) rather than kept as a 16-VGPR tile.
-    const Pk<S> ginh = t == 0 ? zero_pk<S>()
-                              : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
+  if (!(a.ablate & 4)) {
     F pe[Tr<S>::KS];
     {
-      const f32x16 dep = load_cl(a.dEp + ro, c, h);
-      const Pk<S> gEv = load_pk(a.gE + t * fs + ro, c, h);
-      gacc_row<S>(L.gacc + 2 * 1024, L.flush, dep, ginh, lane, wave, tid);
-      gacc_row<S>(L.gacc + 3 * 1024, L.flush, dep, gEv, lane, wave, tid);
+      f32x16 depf;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sm[3] += dep[r];
-      cl_to_pa<S>(wscr, dep, lane, pe);
+      for (int r = 0; r < 16; ++r) depf[r] = (float)dep[r];
+      gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
+      gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, gEv, lane, wave, tid);
+      sm[3] = hsum16(depf);
+      cl_to_pa<S>(wscr, depf, lane, pe);
       const f32x16 dIt0 = a.no_inh ? load_cl(a.dIt + ro, c, h) : zero16();
       const f32x16 dg = gemm_pa<S>(pe, a.gt[5], dIt0, lane);   // no_inh: I_t = gE_t
       store_cl(a.dgEp + ro, c, h, dg);
@@ -737,57 +748,56 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
       const f32x16 dEn = gemm_pa<S>(pe, a.gt[4], load_cl(a.dEn + ro, c, h), lane);
       store_cl(a.dEn + ro, c, h, dEn);
       store_cl(a.dxp + ro, c, h, zero16());
-      continue;
-    }
-    const Pk<S> dIt = load_pk(a.dIt + ro, c, h);
-    const Pk<S> civ = load_pk(a.ci + t * fs + ro, c, h);
-    f32x16 z, xv;
-    stem_cl<ACT>(L.xs, yl, h, st, z, xv);
-    f32x16 g = zero16();
-    {
-      F pax[Tr<S>::KS], pai[Tr<S>::KS];
-      cl_to_pa<S>(wscr, xv, lane, pax);
-      g = gemm_pa<S>(pax, a.gf[2], g, lane);
-      cl_to_pa<S>(wscr, ginh, lane, pai);
-      g = gemm_pa<S>(pai, a.gf[3], g, lane);
-    }
-    f32x16 dIp, dip, dx;
+    } else {
+      f32x16 z, xv;
+      stem_cl<ACT>(L.xs, yl, h, st, z, xv);
+      f32x16 g = zero16();
+      {
+        F pax[Tr<S>::KS], pai[Tr<S>::KS];
+        cl_to_pa<S>(wscr, xv, lane, pax);
+        g = gemm_pa<S>(pax, a.gf[2], g, lane);
+        cl_to_pa<S>(wscr, ginh, lane, pai);
+        g = gemm_pa<S>(pai, a.gf[3], g, lane);
+      }
+      const float A0 = bw0 * rs0, B0 = bb0 - bw0 * rs0 * m0;    // BN0 affine folded
+      f32x16 dIp, dip, dx;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float Ir = (float)ginh[r], dIr = (float)dIt[r];
-      const float xi = ((float)civ[r] - m0) * rs0;
-      const float cn = bw0 * xi + bb0;
-      const float u = al * Ir + mu;
-      const float p = cn * u;
-      float fp, dfp, ih, dfq;
-      Act<ACT>::fd(p, fp, dfp);
-      const float q = xv[r] - fp;
-      Act<ACT>::fd(q, ih, dfq);
-      const float ig = sigm(g[r] + bi);
-      const float dih = dIr * ig;
-      dip[r] = dIr * (ih - Ir) * ig * (1.f - ig);
-      const float dq = dih * dfq;
-      const float dp = -dq * dfp;
-      const float du = dp * cn;
-      const float dci = dp * u;
-      stf(a.dcI + ro + cl_x(r, h) * C + c, dci);
-      dx[r] = dq;
-      dIp[r] = dIr * (1.f - ig) + du * al;
-      sm[0] += du * Ir;
-      sm[1] += du;
-      sm[2] += dip[r];
-      bs0 += dci;
-      bs1 += dci * xi;
+      for (int r = 0; r < 16; ++r) {
+        const float Ir = (float)ginh[r], dIr = (float)dIt[r];
+        const float xi = ((float)civ[r] - m0) * rs0;
+        const float cn = A0 * (float)civ[r] + B0;
+        const float u = al * Ir + mu;
+        const float p = cn * u;
+        float fp, dfp, ih, dfq;
+        Act<ACT>::fd(p, fp, dfp);
+        const float q = xv[r] - fp;
+        Act<ACT>::fd(q, ih, dfq);
+        const float ig = sigm(g[r] + bi);
+        const float dih = dIr * ig;
+        dip[r] = dIr * (ih - Ir) * ig * (1.f - ig);
+        const float dq = dih * dfq;
+        const float dp = -dq * dfp;
+        const float du = dp * cn;
+        const float dci = dp * u;
+        stf(a.dcI + ro + cl_x(r, h) * C + c, dci);
+        dx[r] = dq;
+        dIp[r] = dIr * (1.f - ig) + du * al;
+        sm[0] += du * Ir;
+        sm[1] += du;
+        sm[2] += dip[r];
+        bs0 += dci;
+        bs1 += dci * xi;
+      }
+      gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
+      gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
+      F pd[Tr<S>::KS];
+      cl_to_pa<S>(wscr, dip, lane, pd);
+      dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
+      store_cl(a.dxp + ro, c, h, dx);
+      dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
+      dIp = gemm_pa<S>(pe, a.gt[4], dIp, lane);
+      store_cl(a.GI + ro, c, h, dIp);
     }
-    gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
-    gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
-    F pd[Tr<S>::KS];
-    cl_to_pa<S>(wscr, dip, lane, pd);
-    dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
-    store_cl(a.dxp + ro, c, h, dx);
-    dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
-    dIp = gemm_pa<S>(pe, a.gt[4], dIp, lane);
-    store_cl(a.GI + ro, c, h, dIp);
   }
   sm[4] = bs1;
   sm[5] = bs0;
@@ -1066,6 +1076,26 @@ struct ReduceArgs {
   pt_cell_grads g;
 };
 
+// Deterministic strided sum of n floats (stride in floats) with 16 loads in
+// flight per thread (a serial chain of dependent loads made this kernel
+// latency-bound at ~0.6 ms).
+__device__ __forceinline__ float strided_sum(const float* __restrict__ p, size_t stride, int n) {
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  int i = 0;
+  for (; i + 16 <= n; i += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] += p[(size_t)(i + j) * stride];
+  }
+  for (; i < n; ++i) acc[0] += p[(size_t)i * stride];
+#pragma unroll
+  for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+    for (int j = 0; j < w; ++j) acc[j] += acc[j + w];
+  return acc[0];
+}
+
 __global__ void k_reduce(ReduceArgs r) {
   const int KK = r.K * r.K;
   const int n_small = SLAB;                  // slab entries
@@ -1073,8 +1103,7 @@ __global__ void k_reduce(ReduceArgs r) {
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n_small + n_w;
        e += gridDim.x * blockDim.x) {
     if (e < n_small) {
-      float s = 0.f;
-      for (int b = 0; b < r.B; ++b) s += r.slab[(size_t)b * SLAB + e];
+      const float s = strided_sum(r.slab + e, SLAB, r.B);
       if (e < SLAB_G) {
         const int gate = e / 1024;
         if (r.g.gate_w[gate]) r.g.gate_w[gate][e % 1024] = s;
@@ -1112,8 +1141,8 @@ __global__ void k_reduce(ReduceArgs r) {
       const int e2 = e - n_small;
       const int conv = e2 / (KK * 1024), rem = e2 % (KK * 1024);
       const int tap = rem / 1024, nc = rem % 1024, n = nc / 32, ci = nc % 32;
-      float s = 0.f;
-      for (int gw = 0; gw < r.nwg; ++gw) s += r.wslab[(((size_t)conv * r.nwg + gw) * MAXTAP + tap) * 1024 + nc];
+      const float s = strided_sum(r.wslab + ((size_t)conv * r.nwg * MAXTAP + tap) * 1024 + nc,
+                                  (size_t)MAXTAP * 1024, r.nwg);
       float* W = conv == 0 ? r.g.w_inh : r.g.w_exc;
       if (W) W[(n * C + ci) * KK + tap] = s;
     }
@@ -1434,7 +1463,9 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   if (d->no_inh) { r.g.w_inh = nullptr; r.g.alpha = nullptr; r.g.mu = nullptr;
                    r.g.bn_w[0] = nullptr; r.g.bn_b[0] = nullptr;
                    r.g.gate_w[2] = r.g.gate_w[3] = nullptr; r.g.gate_b[2] = r.g.gate_b[3] = nullptr; }
-  timed(PT_K_REDUCE, st, [&] { hipLaunchKernelGGL(k_reduce, dim3(256), dim3(256), 0, st, r); });
+  const int n_red = SLAB + 2 * p.K * p.K * 1024;              // one thread per output element
+  timed(PT_K_REDUCE, st, [&] {
+    hipLaunchKernelGGL(k_reduce, dim3((n_red + 255) / 256), dim3(256), 0, st, r); });
   HIPCHK(hipGetLastError());
   return 0;
 }
