@@ -47,7 +47,8 @@ struct CellArgs {
   int t;
   int ablate;     // timing experiments only (env PT_CELL_ABLATE): 1 skip conv MFMAs,
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
-                  // atomics, 16 skip LDS weight-grad atomics, 32 skip slab flush
+                  // atomics, 16 skip the 1x1 weight-gradient LDS reductions,
+                  // 32 skip slab flush
   const float* x;                       // [B][3][T][32][32]
   const float *wpre, *bpre;             // [32][3], [32]
   const float *alpha, *mu, *gamma, *kappa;
@@ -315,7 +316,7 @@ constexpr int pw_lds_bytes() {   // forward point-wise kernels use xs, scr, stat
              ? PW_NW * RPP * IMG * 16 + PW_NW * SCR_FLOATS * 4 + 128 * 4
              : PW_NW * RPP * IMG * 16 /*xs*/ + PW_NW * SCR_FLOATS * 4 /*scr*/ + 128 * 4 /*stat*/ +
                    PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ +
-                   PW_NGACC * 1024 * 4 /*gacc*/ + PW_NW * 1024 * 4 /*flush*/;
+                   PW_NGACC * 1024 * 4 /*gacc*/ + PW_NW * 1024 * 4 /*flush*/ + SLAB * 4 /*slab copy*/;
 }
 struct PLds {
   f32x4* xs;
@@ -325,6 +326,7 @@ struct PLds {
   float* red;     // [512]
   float* gacc;    // [PW_NGACC][1024]  (rows n, cols ci)
   float* flush;   // [PW_NW][1024]     per-wave weight-gradient tiles of one gate
+  float* slabl;   // [SLAB]            this workgroup's slab partition, prefetched
 };
 template <int RPP>
 __device__ __forceinline__ PLds pcarve(char* smem) {
@@ -336,6 +338,7 @@ __device__ __forceinline__ PLds pcarve(char* smem) {
   l.red = l.small + PW_NW * NSMALL * 32;
   l.gacc = l.red + 512;
   l.flush = l.gacc + PW_NGACC * 1024;
+  l.slabl = l.flush + PW_NW * 1024;
   return l;
 }
 
@@ -362,16 +365,30 @@ __device__ __forceinline__ void gacc_row(float* gacc_g, float* flush, const f32x
 __device__ void gacc_zero(float* g, int n, int tid) {
   for (int e = tid; e < n * 1024; e += PW_NT) g[e] = 0.f;
 }
-// slab[dst_gate[k]] += gacc[k] for k < n (after a barrier)
-__device__ void gacc_flush(const float* g, float* slab_p, int g0, int n, int tid) {
-  for (int e = tid; e < n * 1024; e += PW_NT) slab_p[(g0 + e / 1024) * 1024 + e % 1024] += g[e];
+// The workgroup's slab partition is copied into LDS by LDS-DMA at kernel
+// start (its latency hides under the staging loads); the flushes at the end
+// then store old + new without waiting on a global read-modify-write.
+__device__ __forceinline__ void slab_prefetch(const float* slab_p, float* slabl, int wave, int lane) {
+  constexpr int NCHUNK = SLAB / 4;                       // 16-B chunks
+  for (int j = wave; j * 64 < NCHUNK; j += PW_NW)
+    if (j * 64 + lane < NCHUNK)
+      __builtin_amdgcn_global_load_lds((const void*)(slab_p + (j * 64 + lane) * 4),
+                                       (__attribute__((address_space(3))) void*)(slabl + j * 256),
+                                       16, 0, 0);
+}
+// slab[g0 + k] = slab copy + gacc[k] for k < n (after a barrier)
+__device__ void gacc_flush(const float* g, const float* slabl, float* slab_p, int g0, int n, int tid) {
+  for (int e = tid; e < n * 1024; e += PW_NT) {
+    const int o = (g0 + e / 1024) * 1024 + e % 1024;
+    slab_p[o] = slabl[o] + g[e];
+  }
 }
 
-// Workgroup sum of per-lane channel values -> slab (RMW, this workgroup's
+// Workgroup sum of per-lane channel values -> slab (this workgroup's
 // partition only: no atomics).
 template <int N>
-__device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, float* slab_p,
-                            int lane, int wave, int tid) {
+__device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, const float* slabl,
+                            float* slab_p, int lane, int wave, int tid) {
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     const float s = v[k] + __shfl_xor(v[k], 32);
@@ -383,7 +400,8 @@ __device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, f
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < PW_NW; ++w) s += small[(w * N + k) * 32 + c];
-    slab_p[SLAB_G + slot[k] * 32 + c] += s;
+    const int o = SLAB_G + slot[k] * 32 + c;
+    slab_p[o] = slabl[o] + s;
   }
   __syncthreads();
 }
@@ -582,6 +600,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   const bool tail = tt <= T - 1, head = t >= 0;
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
+  slab_prefetch(slab_p, L.slabl, wave, lane);
   if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWA_RPP, tid, PW_NT);
   gacc_zero(L.gacc, 2, tid);
   __syncthreads();
@@ -622,8 +641,8 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
           dap[r] = dgE[r] * Et[r] * att[r] * (1.f - att[r]);
           sm[0] += dap[r];
         }
-        gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
-        gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
+        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
+        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
         F pad[Tr<S>::KS];
         cl_to_pa<S>(wscr, dap, lane, pad);
         GE = load_cl(a.dEn + ro, c, h);
@@ -677,8 +696,8 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
   if (head && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * 64, lane, wave, tid);
-  if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, slab_p, lane, wave, tid);   // ends with a barrier
-  if (tail && head && !(a.ablate & 32)) gacc_flush(L.gacc, slab_p, 0, 2, tid);
+  if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
+  if (tail && head && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
 }
 
 // -------------------------------------------------------------------------
@@ -717,6 +736,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
     dIt = load_pk(a.dIt + ro, c, h);
     civ = load_pk(a.ci + t * fs + ro, c, h);
   }
+  slab_prefetch(slab_p, L.slabl, wave, lane);
   stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
   gacc_zero(L.gacc, 4, tid);
   __syncthreads();
@@ -736,8 +756,8 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
       f32x16 depf;
 #pragma unroll
       for (int r = 0; r < 16; ++r) depf[r] = (float)dep[r];
-      gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
-      gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, gEv, lane, wave, tid);
+      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
+      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, gEv, lane, wave, tid);
       sm[3] = hsum16(depf);
       cl_to_pa<S>(wscr, depf, lane, pe);
       const f32x16 dIt0 = a.no_inh ? load_cl(a.dIt + ro, c, h) : zero16();
@@ -788,8 +808,8 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
         bs0 += dci;
         bs1 += dci * xi;
       }
-      gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
-      gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
+      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
+      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
       F pd[Tr<S>::KS];
       cl_to_pa<S>(wscr, dip, lane, pd);
       dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
@@ -803,10 +823,10 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   sm[5] = bs0;
   if (!a.no_inh && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * 64, lane, wave, tid);
   if (a.ablate & 32) return;
-  flush_small<6>(sm, slots, L.small, slab_p, lane, wave, tid);   // ends with a barrier
+  flush_small<6>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5
-  if (!a.no_inh) gacc_flush(L.gacc, slab_p, 2, 2, tid);
-  gacc_flush(L.gacc + 2 * 1024, slab_p, 4, 2, tid);
+  if (!a.no_inh) gacc_flush(L.gacc, L.slabl, slab_p, 2, 2, tid);
+  gacc_flush(L.gacc + 2 * 1024, L.slabl, slab_p, 4, 2, tid);
 }
 
 // D rows per band: 8 (bf16) / 4 (f32, so that two band buffers fit in LDS)

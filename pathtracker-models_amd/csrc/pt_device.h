@@ -199,7 +199,12 @@ __device__ __forceinline__ float hsum16(const f32x16& v) {
 // nl = softplus(beta=1, threshold=20) or tanh (models/InT.py:184, engine.py:145).
 // Hardware exp/log/rcp (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp): absolute
 // deviations from libm are O(1e-7), far inside the 1e-3 parity bound.
-__device__ __forceinline__ float fexp(float x) { return __expf(x); }
+// Raw v_exp_f32 / v_log_f32 (2^x, log2 x): __expf/__logf add a denormal
+// range fix-up (cmp + cndmask + ldexp) around every call; no argument here
+// needs it (results that would be denormal flush to 0, which is harmless for
+// 1 + e^x, sigmoid and tanh).
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float flog(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float sigm(float x) { return frcp(1.f + fexp(-x)); }
 __device__ __forceinline__ float ftanh(float x) {
@@ -213,7 +218,7 @@ __device__ __forceinline__ float ftanh(float x) {
 template <int ACT> struct Act;
 template <> struct Act<0> {
   __device__ static __forceinline__ float f(float x) {
-    const float r = __logf(1.f + fexp(fminf(x, 20.f)));
+    const float r = flog(1.f + fexp(fminf(x, 20.f)));
     return x > 20.f ? x : r;
   }
   __device__ static __forceinline__ float d(float x) {
@@ -225,7 +230,7 @@ template <> struct Act<0> {
   __device__ static __forceinline__ void fd(float x, float& f, float& d) {
     const float e = fexp(fminf(x, 20.f));
     const float s = 1.f + e;
-    const float lf = __logf(s), ld = e * frcp(s);
+    const float lf = flog(s), ld = e * frcp(s);
     f = x > 20.f ? x : lf;
     d = x > 20.f ? 1.f : ld;
   }
