@@ -36,13 +36,14 @@ enum SmallSlot {
 };
 constexpr int SLAB_G = 6 * 1024;                 // 6 gate weights [n][ci]
 constexpr int SLAB = SLAB_G + NSMALL * 32;
-constexpr int NTRANS = 11;                       // backward transients incl. GEfin
+constexpr int NTRANS = 12;                       // backward transients incl. dAt, GEfin
 
 // ----------------------------------------------------------------- arguments
 template <class S>
 struct CellArgs {
   using F = typename Tr<S>::frag;
   int B, T, K, act, no_inh;
+  int hgru;       // hConvGRUCell: the gated inhibition is the attention map (ffhgru_hierarchy.py:147)
   float eps;
   int t;
   int ablate;     // timing experiments only (env PT_CELL_ABLATE): 1 skip conv MFMAs,
@@ -58,11 +59,13 @@ struct CellArgs {
   const F* gf[6];                       // 1x1 fragments, forward
   const F* gt[6];                       // 1x1 fragments, transposed (backward)
   S *E, *I, *gE, *ci, *ce, *eg;         // saved per frame [T][B][32][32][32]
+  S* at;                                // hGRU only: attention map per frame (the gated inhibition)
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
   double* bnacc;                        // fwd BN sums [T][2][3][32]: sum mean_b, sum mean_b^2, sum M2_b
   float* gates;                         // [B][T][C][32][32] or null
   // backward transients, channels-last [B][32][32][32] in the storage type
   S *dEn, *dcE, *dIl, *dEp, *dcI, *GI, *dgEp, *dxp, *dgE, *dIt;
+  S* dAt;                               // hGRU: d loss / d att_t through the gated inhibition
   const float* GEfin;                   // dE of the last frame (channels-last)
   S *dci_s, *dce_s;                     // [T][B][32][32][32] conv-output grads (for k_wgrad)
   double* bnbacc;                       // bwd BN sums [T][2][2][32]: sum dy, sum dy*xhat
@@ -431,7 +434,7 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int 
 //           eg = sig(e_w I_{t-1} + e_u gE) (:171, uses the OLD inhibition;
 //           no_inh: e_w E_{t-1}, :168)
 // -------------------------------------------------------------------------
-template <class S, int ACT>
+template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   static_assert(PWF_RPP == 1, "forward point-wise kernels: one row per wave");
   using F = typename Tr<S>::frag;
@@ -499,8 +502,14 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   }
   F pag[Tr<S>::KS], pai[Tr<S>::KS];
   cl_to_pa<S>(wscr, gEv, lane, pag);
-  if (a.no_inh) cl_to_pa<S>(wscr, Ep, lane, pai);
-  else cl_to_pa<S>(wscr, Iv, lane, pai);
+  if constexpr (HG) {          // g_inh = att (ffhgru_hierarchy.py:147, :154)
+    store_cl(a.at + t * fs + ro, c, h, att);
+    cl_to_pa<S>(wscr, att, lane, pai);
+  } else if (a.no_inh) {
+    cl_to_pa<S>(wscr, Ep, lane, pai);
+  } else {
+    cl_to_pa<S>(wscr, Iv, lane, pai);
+  }
   acc = zero16();
   acc = gemm_pa<S>(pai, a.gf[4], acc, lane);
   acc = gemm_pa<S>(pag, a.gf[5], acc, lane);
@@ -515,7 +524,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
 //   (:162), ig = sig(i_w x + i_u I) (:165), I_t = (1-ig) I + ig Ihat (:166)
 //   [no_inh: I_t = gE (:168)]
 // -------------------------------------------------------------------------
-template <class S, int ACT>
+template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -541,6 +550,9 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   }
   const Pk<S> civ = load_pk(a.ci + t * fs + ro, c, h);
   const Pk<S> Iv = t > 0 ? load_pk(a.I + (t - 1) * fs + ro, c, h) : zero_pk<S>();
+  Pk<S> gi;                    // gated inhibition: I_{t-1} (InT) / att_t (hGRU)
+  if constexpr (HG) gi = load_pk(a.at + t * fs + ro, c, h);
+  else gi = Iv;
   stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
   bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * 96, B, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
@@ -558,11 +570,11 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const float cn = A0 * (float)civ[r] + B0;
-    ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * (float)Iv[r] + mu)));
+    ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * (float)gi[r] + mu)));
   }
   F pax[Tr<S>::KS], pai[Tr<S>::KS];
   cl_to_pa<S>(wscr, xv, lane, pax);
-  cl_to_pa<S>(wscr, Iv, lane, pai);
+  cl_to_pa<S>(wscr, gi, lane, pai);
   f32x16 acc = zero16();
   acc = gemm_pa<S>(pax, a.gf[2], acc, lane);
   acc = gemm_pa<S>(pai, a.gf[3], acc, lane);
@@ -584,7 +596,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
 //     (:175, :173) -> d_eg, dc_e (-> BN1 bwd sums), kappa/gamma grads,
 //     dI_t (local), dE_{t-1} partial = (1-eg) dE_t.
 // -------------------------------------------------------------------------
-template <class S, int ACT>
+template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -625,9 +637,12 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
       f32x16 z, xv;
       stem_cl<ACT>(L.xs, yl, h, st, z, xv);
       f32x16 dx = load_cl(a.dxp + ro, c, h);
-      if (head) {
-        const f32x16 dgE = load_cl(dgsrc + ro, c, h);
-        const f32x16 Et = load_cl(a.E + t * fs + ro, c, h);
+      // attention backward of frame tt.  InT at tt = 0 has none (gE_0 =
+      // att * E_{-1} = 0); hGRU's att_0 still feeds the gated inhibition.
+      if (head || HG) {
+        const f32x16 dgE = head ? load_cl(dgsrc + ro, c, h) : zero16();
+        const Pk<S> dAt = HG ? load_pk(a.dAt + ro, c, h) : zero_pk<S>();
+        const f32x16 Et = head ? load_cl(a.E + t * fs + ro, c, h) : zero16();
         F pax[Tr<S>::KS], pae[Tr<S>::KS];
         cl_to_pa<S>(wscr, xv, lane, pax);
         cl_to_pa<S>(wscr, Et, lane, pae);
@@ -638,17 +653,20 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           att[r] = sigm(g[r] + ba);
-          dap[r] = dgE[r] * Et[r] * att[r] * (1.f - att[r]);
+          const float datt = HG ? dgE[r] * Et[r] + (float)dAt[r] : dgE[r] * Et[r];
+          dap[r] = datt * att[r] * (1.f - att[r]);
           sm[0] += dap[r];
         }
         if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
         if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
         F pad[Tr<S>::KS];
         cl_to_pa<S>(wscr, dap, lane, pad);
-        GE = load_cl(a.dEn + ro, c, h);
+        if (head) {
+          GE = load_cl(a.dEn + ro, c, h);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) GE[r] += dgE[r] * att[r];
-        GE = gemm_pa<S>(pad, a.gt[1], GE, lane);
+          for (int r = 0; r < 16; ++r) GE[r] += dgE[r] * att[r];
+          GE = gemm_pa<S>(pad, a.gt[1], GE, lane);
+        }
         dx = gemm_pa<S>(pad, a.gt[0], dx, lane);
       }
 #pragma unroll
@@ -697,7 +715,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   sm[4] = bs0;   // d bn1.bias   = sum dy
   if (head && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * 64, lane, wave, tid);
   if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
-  if (tail && head && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
+  if (tail && (head || HG) && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
 }
 
 // -------------------------------------------------------------------------
@@ -707,7 +725,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 //   dx_t partial, dI_{t-1}; exc gate backward (:171) -> e_w/e_u grads,
 //   dI_{t-1}, dgE partial.
 // -------------------------------------------------------------------------
-template <class S, int ACT>
+template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   static_assert(PWB_RPP == 1, "k_pw_bb: one row per wave");
   using F = typename Tr<S>::frag;
@@ -727,8 +745,15 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   // (InT) / E_{t-1} (no_inh) and gE_t feed the exc gate (:171), dI_t and c_i
   // the inhibition backward.  Kept packed; e_w^T d_e_pre is folded into
   // dI_{t-1} at the end from its A fragments (pe) rather than kept as a tile.
-  const Pk<S> ginh = t == 0 ? zero_pk<S>()
-                            : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
+  // hGRU: g_inh = att_t (ffhgru_hierarchy.py:147) and I_{t-1} is a separate tile
+  Pk<S> ginh, Iprev;
+  if constexpr (HG) {
+    ginh = load_pk(a.at + t * fs + ro, c, h);
+    Iprev = t == 0 ? zero_pk<S>() : load_pk(a.I + (t - 1) * fs + ro, c, h);
+  } else {
+    ginh = t == 0 ? zero_pk<S>()
+                  : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
+  }
   const Pk<S> dep = load_pk(a.dEp + ro, c, h);
   const Pk<S> gEv = load_pk(a.gE + t * fs + ro, c, h);
   Pk<S> dIt = zero_pk<S>(), civ = zero_pk<S>();
@@ -784,6 +809,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float Ir = (float)ginh[r], dIr = (float)dIt[r];
+        const float Ip = HG ? (float)Iprev[r] : Ir;      // I_{t-1} of the update (:166)
         const float xi = ((float)civ[r] - m0) * rs0;
         const float cn = A0 * (float)civ[r] + B0;
         const float u = al * Ir + mu;
@@ -794,14 +820,17 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
         Act<ACT>::fd(q, ih, dfq);
         const float ig = sigm(g[r] + bi);
         const float dih = dIr * ig;
-        dip[r] = dIr * (ih - Ir) * ig * (1.f - ig);
+        dip[r] = dIr * (ih - Ip) * ig * (1.f - ig);
         const float dq = dih * dfq;
         const float dp = -dq * dfp;
         const float du = dp * cn;
         const float dci = dp * u;
         stf(a.dcI + ro + cl_x(r, h) * C + c, dci);
         dx[r] = dq;
-        dIp[r] = dIr * (1.f - ig) + du * al;
+        // InT: dI_{t-1} collects the update and the gated-inhibition terms;
+        // hGRU: the gated-inhibition terms go to att (dA, kept in dIp's slot)
+        dIp[r] = HG ? du * al : dIr * (1.f - ig) + du * al;
+        if constexpr (HG) Iprev[r] = (S)(dIr * (1.f - ig));
         sm[0] += du * Ir;
         sm[1] += du;
         sm[2] += dip[r];
@@ -816,7 +845,15 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
       store_cl(a.dxp + ro, c, h, dx);
       dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
       dIp = gemm_pa<S>(pe, a.gt[4], dIp, lane);
-      store_cl(a.GI + ro, c, h, dIp);
+      if constexpr (HG) {
+        store_cl(a.dAt + ro, c, h, dIp);
+        f32x16 gi;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gi[r] = (float)Iprev[r];
+        store_cl(a.GI + ro, c, h, gi);
+      } else {
+        store_cl(a.GI + ro, c, h, dIp);
+      }
     }
   }
   sm[4] = bs1;
@@ -1246,7 +1283,7 @@ struct Plan {
   size_t es;          // element size of S
   size_t frame;       // elements per frame tensor (B*NPIX*C)
   // saved offsets
-  size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_bnstat, o_wf[4], o_g[12], saved;
+  size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], saved;
   // workspace offsets
   size_t o_bnacc, o_bnbacc, o_tr[NTRANS], o_dci, o_dce, o_slab, o_wslab, ws;
   int nwg;
@@ -1262,7 +1299,8 @@ int check(const pt_cell_desc* d) {
   if (d->batch < 1 || d->frames < 1) return fail(PT_ERR_ARG, "batch and frames must be >= 1%s%ld");
   if (d->act != PT_ACT_SOFTPLUS && d->act != PT_ACT_TANH) return fail(PT_ERR_ARG, "bad act%s%ld");
   if (d->dtype != PT_DTYPE_F32 && d->dtype != PT_DTYPE_BF16) return fail(PT_ERR_ARG, "bad dtype%s%ld");
-  if (d->cell != PT_CELL_INT) return fail(PT_ERR_UNSUPPORTED, "only the InT cell is built in this version%s%ld");
+  if (d->cell != PT_CELL_INT && d->cell != PT_CELL_HGRU) return fail(PT_ERR_ARG, "bad cell%s%ld");
+  if (d->cell == PT_CELL_HGRU && d->no_inh) return fail(PT_ERR_ARG, "no_inh is an InT option%s%ld");
   return 0;
 }
 
@@ -1279,6 +1317,7 @@ Plan plan(const pt_cell_desc* d) {
   p.o_ci = o; o += fbytes;
   p.o_ce = o; o += fbytes;
   p.o_eg = o; o += fbytes;
+  p.o_at = o; o += d->cell == PT_CELL_HGRU ? fbytes : 0;
   p.o_bnstat = o; o += al((size_t)p.T * 128 * 4);
   for (int i = 0; i < 4; ++i) { p.o_wf[i] = o; o += al((size_t)C * C * MAXTAP * p.es); }
   for (int i = 0; i < 12; ++i) { p.o_g[i] = o; o += al((size_t)C * C * p.es); }
@@ -1302,6 +1341,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
   using F = typename Tr<S>::frag;
   memset(&a, 0, sizeof(a));
   a.B = p.B; a.T = p.T; a.K = p.K; a.act = d->act; a.no_inh = d->no_inh; a.eps = d->eps;
+  a.hgru = d->cell == PT_CELL_HGRU;
   a.x = x;
   {
     const char* ab = getenv("PT_CELL_ABLATE");     // timing experiments only
@@ -1319,12 +1359,13 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
   }
   a.E = (S*)(saved + p.o_E); a.I = (S*)(saved + p.o_I); a.gE = (S*)(saved + p.o_gE);
   a.ci = (S*)(saved + p.o_ci); a.ce = (S*)(saved + p.o_ce); a.eg = (S*)(saved + p.o_eg);
+  a.at = a.hgru ? (S*)(saved + p.o_at) : nullptr;
   a.bnstat = (float*)(saved + p.o_bnstat);
   if (ws) {
     a.bnacc = (double*)(ws + p.o_bnacc);
     a.bnbacc = (double*)(ws + p.o_bnbacc);
     S** tr[NTRANS] = {&a.dEn, &a.dcE, &a.dIl, &a.dEp, &a.dcI, &a.GI, &a.dgEp, &a.dxp,
-                      &a.dgE, &a.dIt, nullptr};
+                      &a.dgE, &a.dIt, &a.dAt, nullptr};
     for (int i = 0; i < NTRANS - 1; ++i) *tr[i] = (S*)(ws + p.o_tr[i]);
     a.GEfin = (const float*)(ws + p.o_tr[NTRANS - 1]);
     a.dci_s = (S*)(ws + p.o_dci); a.dce_s = (S*)(ws + p.o_dce);
@@ -1343,6 +1384,13 @@ void launch_pw(K kern, dim3 grid, size_t lds, hipStream_t st, const A& a) {
   hipLaunchKernelGGL(kern, grid, dim3(PW_NT), lds, st, a);
 }
 
+// (activation, cell) -> kernel instantiation
+#define PW_LAUNCH(kern, grid, lds)                                              \
+  (a.hgru ? (a.act ? launch_pw(kern<S, 1, 1>, grid, lds, st, a)                  \
+                   : launch_pw(kern<S, 0, 1>, grid, lds, st, a))                 \
+          : (a.act ? launch_pw(kern<S, 1, 0>, grid, lds, st, a)                  \
+                   : launch_pw(kern<S, 0, 0>, grid, lds, st, a)))
+
 #define SETLDS(kern, bytes) \
   HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
 
@@ -1353,14 +1401,22 @@ int set_lds_attrs() {
   SETLDS((k_conv<S, FILL_COPY, EPI_FWD>), conv_lds_bytes<S>());
   SETLDS((k_conv<S, FILL_BNBWD, EPI_ADD>), conv_lds_bytes<S>());
   SETLDS((k_conv<S, FILL_BNBWD, EPI_NONE>), conv_lds_bytes<S>());
-  SETLDS((k_pw_fa<S, 0>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_fb<S, 0>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_ba<S, 0>), (pw_lds_bytes<PWA_RPP, true>()));
-  SETLDS((k_pw_bb<S, 0>), (pw_lds_bytes<PWB_RPP, true>()));
-  SETLDS((k_pw_fa<S, 1>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_fb<S, 1>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_ba<S, 1>), (pw_lds_bytes<PWA_RPP, true>()));
-  SETLDS((k_pw_bb<S, 1>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_fa<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_fb<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_ba<S, 0, 0>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_bb<S, 0, 0>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_fa<S, 0, 1>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_fb<S, 0, 1>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_ba<S, 0, 1>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_bb<S, 0, 1>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_fa<S, 1, 0>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_fb<S, 1, 0>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_ba<S, 1, 0>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_bb<S, 1, 0>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_fa<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_fb<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
+  SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_bb<S, 1, 1>), (pw_lds_bytes<PWB_RPP, true>()));
   SETLDS(k_wgrad<S>, wgrad_lds_bytes<S>());
   done = true;
   return 0;
@@ -1401,14 +1457,14 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   cb.wf = a.wf_exc;
   for (int t = 0; t <= p.T; ++t) {
     a.t = t;
-    timed(PT_K_PW_FA, st, [&] { (a.act ? launch_pw(k_pw_fa<S, 1>, gpf, lpf, st, a) : launch_pw(k_pw_fa<S, 0>, gpf, lpf, st, a)); });
+    timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });
     if (t == p.T) break;
     if (!d->no_inh) {
       ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * 96;
       timed(PT_K_CONV_FA, st, [&] {
         hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, ca); });
     }
-    timed(PT_K_PW_FB, st, [&] { (a.act ? launch_pw(k_pw_fb<S, 1>, gpf, lpf, st, a) : launch_pw(k_pw_fb<S, 0>, gpf, lpf, st, a)); });
+    timed(PT_K_PW_FB, st, [&] { PW_LAUNCH(k_pw_fb, gpf, lpf); });
     cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * 96;
     timed(PT_K_CONV_FB, st, [&] {
       hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, cb); });
@@ -1439,7 +1495,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   const float* bst = a.bnstat;
   a.t = p.T - 1;
   a.conv_done = 0;
-  timed(PT_K_PW_BA, st, [&] { (a.act ? launch_pw(k_pw_ba<S, 1>, gpa, lpa, st, a) : launch_pw(k_pw_ba<S, 0>, gpa, lpa, st, a)); });
+  timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
   for (int t = p.T - 1; t >= 0; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
@@ -1449,7 +1505,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
     timed(PT_K_CONV_BB, st, [&] {
       hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_ADD>), dim3(p.B), dim3(NT), lcv, st, cb); });
     a.t = t;
-    timed(PT_K_PW_BB, st, [&] { (a.act ? launch_pw(k_pw_bb<S, 1>, gpb, lpb, st, a) : launch_pw(k_pw_bb<S, 0>, gpb, lpb, st, a)); });
+    timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
     a.conv_done = 0;
     if (!d->no_inh) {
       // dgE_t = conv^T(BN0-bwd(dcI), w_inh) + e_u^T d_e_pre ; frame 0's conv^T is dead (E_{-1}=0)
@@ -1467,7 +1523,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
       }
     }
     a.t = t - 1;
-    timed(PT_K_PW_BA, st, [&] { (a.act ? launch_pw(k_pw_ba<S, 1>, gpa, lpa, st, a) : launch_pw(k_pw_ba<S, 0>, gpa, lpa, st, a)); });
+    timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
   }
   float* wslab = (float*)((char*)ws + p.o_wslab);
   const int conv0 = d->no_inh ? 1 : 0;

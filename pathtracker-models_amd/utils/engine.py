@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from models import InT
+from models import ffhgru_hierarchy
 
 TORCHVISION = ['r3d', 'mc3', 'r2plus1', 'nostride_r3d', 'nostride_r3d_pos']
 SLOWFAST = ['slowfast', 'slowfast_nl']
@@ -62,7 +63,15 @@ def model_step(model, imgs, model_name, test=False):
 
 
 def model_selector(args, timesteps, device, fb_kernel_size=7, dimensions=32):
-    """Construct a model by name (utils/engine.py:77-146; InT variants)."""
+    """Construct a model by name (utils/engine.py:77-146; InT variants).
+
+    'ffhgru' (not registered by the reference's engine, whose 'hgru' entry
+    imports the absent models/hgrucleanSEG.py) builds
+    models/ffhgru_hierarchy.py's FFhGRU."""
+    if args.model == 'ffhgru':
+        return ffhgru_hierarchy.FFhGRU(dimensions=dimensions, timesteps=timesteps,
+                                       kernel_size=fb_kernel_size, jacobian_penalty=False,
+                                       grad_method='bptt')
     extra = INT_VARIANTS.get(args.model)
     if extra is None:
         raise NotImplementedError("Model not found.")

@@ -133,7 +133,7 @@ def make_int(ref_int, tag, *, batch, t_len, dims, act="softplus", no_inh=False,
           "loss", float(out["loss"]))
 
 
-def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0):
+def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0, want_gates=True):
     synth = _synth()
     torch.manual_seed(2000 + seed)
     model = ref_hgru.FFhGRU(dimensions=dims, timesteps=t_len, kernel_size=7,
@@ -141,7 +141,7 @@ def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0):
     perturb_recurrent(model, seed)
     clips, labels = synth.make_batch(seed + 7, batch, t_len)
     x, y = prepare(clips, labels)
-    out = run_recurrent(model, x, y, True)
+    out = run_recurrent(model, x, y, want_gates)
     out.update(clip_u8=clips, label_u8=np.array([ord(b) for b in labels], np.uint8),
                cfg_cell=np.array("hgru"), cfg_act=np.array("softplus"), cfg_no_inh=np.array(False),
                cfg_lesion=np.array(""), cfg_dims=np.array(dims), cfg_k=np.array(7))
@@ -194,6 +194,16 @@ def make_init(ref_int, tag, seed=123):
     print(tag, len(sd), "tensors")
 
 
+def make_init_hgru(ref_hgru, tag, seed=123):
+    """FFhGRU initial parameters under a fixed seed (its own registration / RNG order)."""
+    torch.manual_seed(seed)
+    model = ref_hgru.FFhGRU(dimensions=32, timesteps=8, kernel_size=7, jacobian_penalty=False,
+                            grad_method="bptt")
+    sd = {k: v.numpy() for k, v in model.state_dict().items() if k != "unit1.w"}
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **sd)
+    print(tag, len(sd), "tensors")
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not mounted; golden vectors are generated in the build container only")
@@ -208,18 +218,29 @@ def main():
         ref_hgru = _load("ref_ffhgru", os.path.join(REF, "models", "ffhgru_hierarchy.py"))
         ref_clstm = _load("ref_convlstm", os.path.join(REF, "models", "convlstm.py"))
 
-        make_init(ref_int, "init_seed123")
-        if os.environ.get("GOLDEN_ONLY_INIT"):
-            return
-        make_int(ref_int, "int_tiny_c8", batch=2, t_len=8, dims=8)
-        make_int(ref_int, "int_c32", batch=2, t_len=8, dims=32, seed=1)
-        make_int(ref_int, "int_noinh", batch=2, t_len=8, dims=32, no_inh=True, seed=2)
-        make_int(ref_int, "int_tanh", batch=2, t_len=8, dims=32, act="tanh", seed=3)
-        make_int(ref_int, "int_lesion", batch=2, t_len=6, dims=32, lesion=("alpha", "gamma"),
-                 seed=4)
-        make_int(ref_int, "int_cfg1", batch=4, t_len=32, dims=32, want_gates=False, seed=5)
-        make_hgru(ref_hgru, "hgru_c32", batch=2, t_len=6, dims=32, seed=6)
-        make_convlstm(ref_clstm, "convlstm_k7", batch=2, timesteps=4, filt=7, seed=7)
+        jobs = {
+            "init_seed123": lambda: make_init(ref_int, "init_seed123"),
+            "init_hgru_seed123": lambda: make_init_hgru(ref_hgru, "init_hgru_seed123"),
+            "int_tiny_c8": lambda: make_int(ref_int, "int_tiny_c8", batch=2, t_len=8, dims=8),
+            "int_c32": lambda: make_int(ref_int, "int_c32", batch=2, t_len=8, dims=32, seed=1),
+            "int_noinh": lambda: make_int(ref_int, "int_noinh", batch=2, t_len=8, dims=32,
+                                          no_inh=True, seed=2),
+            "int_tanh": lambda: make_int(ref_int, "int_tanh", batch=2, t_len=8, dims=32,
+                                         act="tanh", seed=3),
+            "int_lesion": lambda: make_int(ref_int, "int_lesion", batch=2, t_len=6, dims=32,
+                                           lesion=("alpha", "gamma"), seed=4),
+            "int_cfg1": lambda: make_int(ref_int, "int_cfg1", batch=4, t_len=32, dims=32,
+                                         want_gates=False, seed=5),
+            "hgru_c32": lambda: make_hgru(ref_hgru, "hgru_c32", batch=2, t_len=6, dims=32, seed=6),
+            "hgru_b4t16": lambda: make_hgru(ref_hgru, "hgru_b4t16", batch=4, t_len=16, dims=32,
+                                            seed=8, want_gates=False),
+            "convlstm_k7": lambda: make_convlstm(ref_clstm, "convlstm_k7", batch=2, timesteps=4,
+                                                 filt=7, seed=7),
+        }
+        only = os.environ.get("GOLDEN_ONLY")          # comma-separated tags to (re)generate
+        for tag, job in jobs.items():
+            if not only or tag in only.split(","):
+                job()
     finally:
         torch.Tensor.cuda = orig_cuda
 

@@ -15,6 +15,7 @@ from goldens import cfg, load, params, prepared_input
 pytestmark = pytest.mark.gpu
 
 INT_TAGS = ["int_c32", "int_tanh", "int_lesion", "int_noinh", "int_cfg1"]
+HGRU_TAGS = ["hgru_c32", "hgru_b4t16"]
 
 
 def _dev():
@@ -27,6 +28,12 @@ def _model(g, dtype="f32"):
     from models import InT as int_mod
     import torch.nn.functional as F
     c = cfg(g)
+    if c["cell"] == "hgru":
+        from models import ffhgru_hierarchy as hg
+        m = hg.FFhGRU(dimensions=c["dims"], timesteps=8, kernel_size=7)
+        m.load_state_dict(params(g), strict=True)
+        m.cell_dtype = dtype
+        return m
     kw = dict(dimensions=c["dims"], timesteps=8, kernel_size=7, no_inh=c["no_inh"],
               nl=F.tanh if c["act"] == "tanh" else F.softplus)
     for les in c["lesion"]:
@@ -50,7 +57,7 @@ def _assert_close(name, a, b, atol, rtol=0.0):
     assert e <= atol + rtol * s, f"{name}: max|err| {e:.3e} > {atol:.1e} + {rtol:.1e}*{s:.3e}"
 
 
-@pytest.mark.parametrize("tag", INT_TAGS)
+@pytest.mark.parametrize("tag", INT_TAGS + HGRU_TAGS)
 def test_forward_testmode_f32(tag):
     dev = _dev()
     g = load(tag)
@@ -67,7 +74,7 @@ def test_forward_testmode_f32(tag):
     assert np.array_equal(logits.cpu().numpy() > 0, g["logits"] > 0)
 
 
-@pytest.mark.parametrize("tag", INT_TAGS)
+@pytest.mark.parametrize("tag", INT_TAGS + HGRU_TAGS)
 def test_bptt_grads_and_adam_f32(tag):
     dev = _dev()
     g = load(tag)
@@ -94,7 +101,7 @@ def test_bptt_grads_and_adam_f32(tag):
         _assert_close(f"adam {k}", p.detach().cpu(), g["adam." + k], 1e-6, 1e-3)
 
 
-@pytest.mark.parametrize("tag", ["int_c32", "int_cfg1"])
+@pytest.mark.parametrize("tag", ["int_c32", "int_cfg1", "hgru_c32"])
 def test_forward_bf16_tolerance(tag):
     """bf16 operands / saved states, f32 accumulation: logits within 5e-2 and
     per-frame states within 5e-2 of the reference after up to 32 recurrent steps."""
@@ -108,11 +115,12 @@ def test_forward_bf16_tolerance(tag):
     _assert_close("bf16 states", states.cpu(), g["states"], 5e-2, 5e-2)
 
 
-def test_bf16_grads_direction():
+@pytest.mark.parametrize("tag", ["int_c32", "hgru_c32"])
+def test_bf16_grads_direction(tag):
     """bf16 BPTT gradients point the same way as the reference's (cosine > 0.99
     per parameter tensor with a non-trivial gradient)."""
     dev = _dev()
-    g = load("int_c32")
+    g = load(tag)
     m = _model(g, "bf16").to(dev)
     x, y = prepared_input(g)
     out, _ = m(x.to(dev))

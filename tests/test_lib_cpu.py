@@ -80,6 +80,21 @@ def test_init_matches_reference_rng_order():
         np.testing.assert_array_equal(sd[k].numpy(), z[k], err_msg=k)
 
 
+def test_hgru_init_and_keys_match_reference():
+    """FFhGRU drop-in: state_dict keys in the reference order and the initial
+    values under seed 123 bit-identical (models/ffhgru_hierarchy.py:58-207)."""
+    from models import ffhgru_hierarchy as hg
+    z = np.load(os.path.join(GOLDEN, "init_hgru_seed123.npz"), allow_pickle=False)
+    torch.manual_seed(123)
+    m = hg.FFhGRU(dimensions=32, timesteps=8, kernel_size=7)
+    sd = m.state_dict()
+    assert [k for k in sd if k != "unit1.w"] == list(z.files)
+    for k in z.files:
+        np.testing.assert_array_equal(sd[k].numpy(), z[k], err_msg=k)
+    g = np.load(os.path.join(GOLDEN, "hgru_c32.npz"), allow_pickle=False)
+    assert list(sd) == [k[len("param."):] for k in g.files if k.startswith("param.")]
+
+
 def test_lesion_freezes_only_named_params():
     from models import InT as int_mod
     m = int_mod.InT(dimensions=32, kernel_size=7, lesion_alpha=True, lesion_gamma=True)
