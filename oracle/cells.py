@@ -168,13 +168,16 @@ def adam_step(params: Params, grads: Params, lr: float = 3e-4, betas=(0.9, 0.999
 
 # ----------------------------------------------------------------------------- ConvLSTM
 
-def convlstm_forward(sd: Params, img: Tensor, timesteps: int, eps: float = 1e-3):
+def convlstm_forward(sd: Params, img: Tensor, timesteps: int, eps: float = 1e-3,
+                     with_jv: bool = False, mu: float = 0.9):
     """ConvLSTM on a static single-channel image (models/convlstm.py:116-147, bptt).
 
     conv0 (Gabor 7x7, 1->25, bias) then ``pow 2`` (:118-119); ``timesteps``
     iterations of the 4-gate cell on the same x (:137-139, cell :84-90; x-convs
     with bias, h-convs without); ``BN(h)`` (batch stats, :111,146) -> 1x1
-    ``conv6`` 25->2 (:112,147).  Returns ``(output [B,2,H,W], h_T, c_T)``.
+    ``conv6`` 25->2 (:112,147).  Returns ``(output [B,2,H,W], h_T, c_T)``, or
+    ``(output, h_T, c_T, jv_penalty)`` with ``with_jv`` (see
+    :func:`convlstm_jv_penalty`).
     """
     x = F.conv2d(img, sd["conv0.weight"], sd["conv0.bias"], padding=3).pow(2)
     k = sd["unit1.Wxi.weight"].shape[-1]
@@ -188,15 +191,38 @@ def convlstm_forward(sd: Params, img: Tensor, timesteps: int, eps: float = 1e-3)
     def hconv(g, v):
         return F.conv2d(v, sd[f"unit1.Wh{g}.weight"], None, padding=pad)
 
+    hs, cs = [], []
     for _ in range(timesteps):
         i_t = torch.sigmoid(xconv("i", x) + hconv("i", h))
         f_t = torch.sigmoid(xconv("f", x) + hconv("f", h))
         c = f_t * c + i_t * torch.tanh(xconv("c", x) + hconv("c", h))
         o_t = torch.sigmoid(xconv("o", x) + hconv("o", h))
         h = o_t * torch.tanh(c)
+        hs.append(h)
+        cs.append(c)
     out = F.batch_norm(h, None, None, sd["bn.weight"], sd["bn.bias"], training=True, eps=eps)
     out = F.conv2d(out, sd["conv6.weight"], sd["conv6.bias"])
-    return out, h, c
+    if not with_jv:
+        return out, h, c
+    return out, h, c, convlstm_jv_penalty(hs, cs, mu)
+
+
+def convlstm_jv_penalty(hs, cs, mu: float = 0.9) -> Tensor:
+    """Training-mode Jacobian penalty of ConvLSTM (models/convlstm.py:150-161, l1):
+
+        jv = clamp(J_h^T 1 - mu, 0)^2 + clamp(J_c^T 1 - mu, 0)^2
+
+    with J_h = d h_{T-1} / d h_{T-2} (the one-step path through the h-convs) and
+    J_c = d c_{T-1} / d c_{T-2}, which autograd takes along EVERY path: the
+    direct forget-gate term f_{T-1} and the path through h_{T-2} = o tanh(c_{T-2})
+    into the next step's gates.  ``hs`` / ``cs`` are the per-step states of a
+    graph that requires grad; needs ``timesteps >= 2`` (the reference's
+    ``state_2nd_last`` is unbound otherwise).
+    """
+    ones = torch.ones_like(hs[-1])
+    jh = torch.autograd.grad(hs[-1], hs[-2], ones, retain_graph=True)[0]
+    jc = torch.autograd.grad(cs[-1], cs[-2], ones, retain_graph=True)[0]
+    return ((jh - mu).clamp(0) ** 2 + (jc - mu).clamp(0) ** 2).detach()
 
 
 def flops_per_clip_frame(c: int = 32, h: int = 32, w: int = 32, k: int = 7) -> int:

@@ -236,6 +236,12 @@ def main():
                                             seed=8, want_gates=False),
             "convlstm_k7": lambda: make_convlstm(ref_clstm, "convlstm_k7", batch=2, timesteps=4,
                                                  filt=7, seed=7),
+            # the reference default filt_size=15 (convlstm.py:95) and the shortest
+            # unroll that has a state_2nd_last (T=2, convlstm.py:140-143)
+            "convlstm_k15": lambda: make_convlstm(ref_clstm, "convlstm_k15", batch=2,
+                                                  timesteps=3, filt=15, seed=9),
+            "convlstm_t2": lambda: make_convlstm(ref_clstm, "convlstm_t2", batch=3, timesteps=2,
+                                                 filt=7, seed=10),
         }
         only = os.environ.get("GOLDEN_ONLY")          # comma-separated tags to (re)generate
         for tag, job in jobs.items():

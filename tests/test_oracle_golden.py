@@ -71,8 +71,9 @@ def test_recurrent_bptt_grads_and_adam(tag):
         _close(stepped[k], g["adam." + k], rtol=1e-5, atol=1e-6)
 
 
-def test_convlstm_static():
-    g = load("convlstm_k7")
+@pytest.mark.parametrize("tag", ["convlstm_k7", "convlstm_k15", "convlstm_t2"])
+def test_convlstm_static(tag):
+    g = load(tag)
     sd = params(g)
     img = torch.from_numpy(g["img"])
     target = torch.from_numpy(g["target"])
@@ -81,7 +82,8 @@ def test_convlstm_static():
         out, _, _ = cells.convlstm_forward(sd, img, steps)
     _close(out, g["eval_output"])
     leaf = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
-    out, _, _ = cells.convlstm_forward(leaf, img, steps)
+    out, _, _, jv = cells.convlstm_forward(leaf, img, steps, with_jv=True)
+    _close(jv, g["jv_penalty"], rtol=1e-4, atol=1e-6)
     loss = torch.nn.functional.cross_entropy(out, target)
     loss.backward()
     _close(loss.item(), float(g["loss"]))
