@@ -1,0 +1,97 @@
+/*
+ * pt_lstm.h — C ABI of the MI355X (gfx950) ConvLSTM cell library (libptlstm.so).
+ *
+ * Drop-in boundary beneath the reference's ConvLSTM (models/convlstm.py):
+ *   ConvLSTMCell.forward   models/convlstm.py:84-90   (one step, x/h/c given)
+ *   ConvLSTM.forward loop  models/convlstm.py:137-143 (bptt: `timesteps` steps
+ *                                                     on a static x, h0=c0=0)
+ *   autograd BPTT through that loop, and the training-mode Jacobian penalty
+ *   models/convlstm.py:150-161 (l1: two vector-Jacobian products).
+ * conv0 + pow2 (:118-119), BN (:146) and conv6 (:147) stay in PyTorch; the
+ * library takes the squared conv0 output x and returns h (and c).
+ *
+ * Conventions as include/pt_cell.h: plain C types, caller-owned buffers (fp32
+ * NCHW tensors in their PyTorch layout, an opaque saved blob and workspace),
+ * an explicit stream per call, no mutable global state, int status with a
+ * thread-local message (pt_lstm_last_error()).
+ *
+ * Gate order everywhere is the reference's attribute order i, f, c, o
+ * (Wxi/Whi, Wxf/Whf, Wxc/Whc, Wxo/Who, models/convlstm.py:63-73).
+ */
+#ifndef PT_LSTM_H
+#define PT_LSTM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* pt_lstm_stream_t;   /* == hipStream_t */
+
+enum { PT_LSTM_OK = 0, PT_LSTM_ERR_ARG = 1, PT_LSTM_ERR_UNSUPPORTED = 2, PT_LSTM_ERR_HIP = 3 };
+enum { PT_LSTM_F32 = 0, PT_LSTM_BF16 = 1 };      /* storage + MFMA operand type */
+enum { PT_LSTM_H0 = 1, PT_LSTM_C0 = 2 };         /* desc.init_state bits        */
+
+typedef struct pt_lstm_desc {
+    int32_t batch;        /* B images                                          */
+    int32_t in_channels;  /* input_channels  (25 in ConvLSTM), <= 32           */
+    int32_t channels;     /* hidden_channels (25 in ConvLSTM), <= 32           */
+    int32_t height;       /* H (32)                                            */
+    int32_t width;        /* W (32)                                            */
+    int32_t ksize;        /* kernel_size, odd, <= 15 (filt_size, default 15)   */
+    int32_t steps;        /* recurrent steps T (timesteps), >= 1               */
+    int32_t dtype;        /* PT_LSTM_F32 / PT_LSTM_BF16                        */
+    int32_t init_state;   /* PT_LSTM_H0 | PT_LSTM_C0: initial h / c are given  */
+} pt_lstm_desc;
+
+/* fp32, PyTorch layouts: wx[g] [ch,cin,k,k], bx[g] [ch], wh[g] [ch,ch,k,k]. */
+typedef struct pt_lstm_params {
+    const float* wx[4];
+    const float* bx[4];
+    const float* wh[4];
+} pt_lstm_params;
+
+/* Gradients (fp32, overwritten; any pointer may be NULL).  d_x [B,cin,H,W];
+ * d_h0 / d_c0 [B,ch,H,W] (only meaningful when h0 / c0 were given). */
+typedef struct pt_lstm_grads {
+    float* wx[4];
+    float* bx[4];
+    float* wh[4];
+    float* d_x;
+    float* d_h0;
+    float* d_c0;
+} pt_lstm_grads;
+
+size_t pt_lstm_saved_bytes(const pt_lstm_desc* d);
+size_t pt_lstm_workspace_bytes(const pt_lstm_desc* d);
+
+/* T steps of the cell on a static x [B,cin,H,W] from (h0, c0) [B,ch,H,W]
+ * (NULL = zeros, as convlstm.py:120-121; must agree with desc.init_state).
+ * Writes h_T, c_T [B,ch,H,W] (either may be NULL) and keeps everything the
+ * backward / jv calls need in `saved` (prepared weight fragments included). */
+int pt_lstm_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* p,
+                    const float* h0, const float* c0, void* saved, float* h_out, float* c_out,
+                    pt_lstm_stream_t stream);
+
+/* BPTT from dL/dh_T (d_h, required) and dL/dc_T (d_c, NULL = 0), using the
+ * `saved` blob of the matching forward. */
+int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace,
+                     const float* d_h, const float* d_c, const pt_lstm_grads* g,
+                     pt_lstm_stream_t stream);
+
+/* Training-mode Jacobian penalty of the last step (convlstm.py:150-161, l1):
+ *   jv = clamp(J_h^T 1 - mu, 0)^2 + clamp(J_c^T 1 - mu, 0)^2      [B,ch,H,W]
+ * J_h = dh_{T-1}/dh_{T-2}; J_c = dc_{T-1}/dc_{T-2} along every path (the forget
+ * gate and the path through h_{T-2}).  Needs steps >= 2. */
+int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace, float mu,
+                       float* jv, pt_lstm_stream_t stream);
+
+const char* pt_lstm_last_error(void);
+const char* pt_lstm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_LSTM_H */

@@ -1,0 +1,963 @@
+// pt_lstm.hip — ConvLSTM cell (models/convlstm.py) forward + BPTT for MI355X (gfx950).
+//
+// Reference path replaced (paths relative to the reference repo):
+//   ConvLSTMCell.forward  models/convlstm.py:84-90     one step: 8 k x k convs + gates
+//   ConvLSTM bptt loop    models/convlstm.py:137-143   `timesteps` steps on a static x
+//   autograd BPTT         (loss.backward through that loop)
+//   Jacobian penalty      models/convlstm.py:150-161   two one-step VJPs
+//
+// x is static over the steps, so its four gate convolutions are computed ONCE
+// (xg = Wx * x + b, N = 4 gates x 32 padded channels = 128) and every step adds
+// the h convolution P_t = xg + Wh * h_{t-1} from one implicit-GEMM kernel whose
+// four waves each own one gate tile (k_lconv<.., NI=1, NO=4>).  The gate
+// non-linearities and the c / h update are a point-wise kernel (k_lpw_fwd).
+// BPTT runs the same conv kernel transposed (Wh^T, 4 gates in, 32 out,
+// k_lconv<.., NI=4, NO=1>), a point-wise backward (k_lpw_bwd), and one
+// weight-gradient kernel per conv family over all (step, image) pairs
+// (k_lwgrad).  Because x is static, dWx and dx need only sum_t dP_t.
+//
+// Layouts (channels-last, channels padded to 32 per gate; padded channels stay
+// exactly zero: zero weights / bias give P = 0 -> c stays 0, h = 0.5 tanh 0 = 0):
+//   x_cl  [B][1024][32] S         xg, P_t [B][1024][128] f32 (gate g at 32 g)
+//   h_t   [T][B][1024][32] S      c_t     [T][B][1024][32] f32
+//   dP_t  [T][B][1024][128] S     dPsum   [B][1024][128] f32 (+ an S copy)
+// Conv kernels tile the 32x32 image in 4 bands of 8 output rows; the band plus
+// its (k-1)-row / (k-1)-column zero halo is one LDS tile (22 x 46 x 32 bf16 =
+// 63 KB at k = 15).
+#include "pt_device.h"
+#include "../../include/pt_lstm.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+namespace ptl {
+using namespace ptc;
+
+constexpr int HC = 32;             // padded hidden / input channels
+constexpr int NG = 4;              // gates i, f, c, o
+constexpr int GC = NG * HC;        // 128
+constexpr int RB = 8;              // output rows per conv band
+constexpr int NBAND = IMG / RB;    // 4
+constexpr int KMAX = 15;
+
+// ------------------------------------------------------------------ conv tile
+template <class S, int K> struct LTile {
+  static constexpr int P = K / 2;
+  static constexpr int TR = RB + K - 1;      // tile rows
+  static constexpr int TC = IMG + K - 1;     // tile columns
+  static constexpr int CP = Tr<S>::CP;       // channels per pass in LDS
+  static constexpr int BYTES = TR * TC * CP * (int)sizeof(S);
+  // bf16: 16-B chunks of 8 channels XOR-swizzled by (col >> 2) & 3 so the 32
+  // lanes of a B-fragment read (consecutive columns) spread over bank groups
+  __device__ static __forceinline__ int off(int trow, int tcol, int ch) {
+    if constexpr (sizeof(S) == 4) {
+      return (trow * TC + tcol) * CP + ch;
+    } else {
+      return (trow * TC + tcol) * 32 + ((((ch >> 3) ^ ((tcol >> 2) & 3))) << 3) + (ch & 7);
+    }
+  }
+};
+
+struct LConvArgs {
+  const void* src;      // S [nimg][NPIX][32*NI]
+  const void* wf;       // fragments [NO][NI][K*K][KS][64]
+  float* out;           // f32 [nimg][NPIX][32*NO]
+  const float* add;     // f32, same layout as out, or null
+  const float* bias;    // f32 [32*NO] or null
+  int nimg;
+};
+
+// out[img][p][32 o + n] = sum_{ig, ci, tap} W[o, ig][n][ci][tap] src[img][p + tap][32 ig + ci]
+//                          (+ add) (+ bias)
+// Weights on the MFMA A side, pixels on B: the result is in the PL layout
+// (lane = pixel) and leaves with 16-B vector stores.  Column-tap-major loop
+// with row reuse as in pt_device.h conv_run_k: each B fragment (tile row,
+// kw, k-step) is read from LDS once and feeds the K MFMAs of the output rows
+// it contributes to.  Wave w: output tile o = w % NO, rows (w / NO) * RW ...
+template <class S, int K, int NI, int NO>
+__global__ __launch_bounds__(NT, 1) void k_lconv(LConvArgs a) {
+  using TT = Tr<S>;
+  using F = typename TT::frag;
+  using L = LTile<S, K>;
+  constexpr int KK = K * K;
+  constexpr int KSP = TT::KS / TT::NPASS;
+  constexpr int RW = RB * NO / NWAVE;        // 8 (NO = 4) or 2 (NO = 1)
+  constexpr int NTR = RW + K - 1;
+  constexpr int CPB = 16 / (int)sizeof(S);   // channels per 16-B chunk
+  constexpr int NCH = L::CP / CPB;           // chunks per pixel per pass (4)
+  constexpr int NCHUNK = L::TR * IMG * NCH;
+  constexpr int PER = (NCHUNK + NT - 1) / NT;
+  constexpr int SRCC = 32 * NI;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  S* tile = (S*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, px = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int img = blockIdx.x / NBAND, band = blockIdx.x % NBAND, y0 = band * RB;
+  const int o = wave % NO, r0 = (wave / NO) * RW;
+  const S* src = (const S*)a.src + (size_t)img * NPIX * SRCC;
+  const F* wf = (const F*)a.wf;
+
+  for (int i = tid; i < L::BYTES / 16; i += NT) ((u32x4*)tile)[i] = u32x4{0u, 0u, 0u, 0u};
+
+  f32x16 acc[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) acc[i] = zero16();
+
+  for (int ig = 0; ig < NI; ++ig) {
+    for (int pass = 0; pass < TT::NPASS; ++pass) {
+      // ---- fill the band tile (rows outside the image are written as zeros;
+      // the halo columns stay zero from the initial clear)
+      u32x4 v[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx0 = tid + k * NT;
+        const int idx = idx0 < NCHUNK ? idx0 : NCHUNK - 1;
+        const int q = idx % NCH, pc = idx / NCH, col = pc % IMG, row = pc / IMG;
+        const int iy = y0 + row - L::P;
+        const int cy = iy < 0 ? 0 : (iy >= IMG ? IMG - 1 : iy);
+        v[k] = *(const u32x4*)(src + (size_t)(cy * IMG + col) * SRCC + ig * 32 + pass * L::CP +
+                               q * CPB);
+        if (iy != cy) v[k] = u32x4{0u, 0u, 0u, 0u};
+      }
+      __syncthreads();   // the previous pass's fragment reads are done
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = tid + k * NT;
+        if (PER * NT == NCHUNK || idx < NCHUNK) {
+          const int q = idx % NCH, pc = idx / NCH, col = pc % IMG, row = pc / IMG;
+          *(u32x4*)(tile + L::off(row, col + L::P, q * CPB)) = v[k];
+        }
+      }
+      __syncthreads();
+
+      for (int kw = 0; kw < K; ++kw) {
+        F bc[K][KSP];
+        const F* wk = wf + ((size_t)((o * NI + ig) * KK + kw) * TT::KS + pass * KSP) * 64 + lane;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+          for (int s = 0; s < KSP; ++s) bc[kh][s] = wk[((size_t)kh * K * TT::KS + s) * 64];
+        const int tcol = px + kw;
+        F av[NTR][KSP];
+        auto load_a = [&](int tr) {
+          const int trow = r0 + tr;
+#pragma unroll
+          for (int s = 0; s < KSP; ++s) {
+            if constexpr (sizeof(S) == 4) {
+              av[tr][s] = tile[L::off(trow, tcol, 2 * s + h)];
+            } else {
+              av[tr][s] = *(const bf16x8*)(tile + L::off(trow, tcol, 16 * s + 8 * h));
+            }
+          }
+        };
+        constexpr int PF = 3 < NTR ? 3 : NTR;
+#pragma unroll
+        for (int tr = 0; tr < PF; ++tr) load_a(tr);
+#pragma unroll
+        for (int tr = 0; tr < NTR; ++tr) {
+          if (tr + PF < NTR) load_a(tr + PF);
+#pragma unroll
+          for (int s = 0; s < KSP; ++s) {
+#pragma unroll
+            for (int kh = 0; kh < K; ++kh) {
+              const int i = tr - kh;
+              if (i >= 0 && i < RW) acc[i] = TT::mma(bc[kh][s], av[tr][s], acc[i]);
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: PL layout, lane = pixel, register r = channel pl_ch(r, h)
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int y = y0 + r0 + i;
+    const size_t po = ((size_t)img * NPIX + y * IMG + px) * (32 * NO) + o * 32;
+    f32x16 v = acc[i];
+    if (a.add) add_pl(a.add + po, h, v);
+    if (a.bias) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] += a.bias[o * 32 + pl_ch(r, h)];
+    }
+    store_pl(a.out + po, h, v);
+  }
+}
+
+// ------------------------------------------------------------- point-wise
+// One thread per (pixel, 4-channel quad).  Gates (models/convlstm.py:85-89):
+//   i = sig(P_i)  f = sig(P_f)  g = tanh(P_c)  o = sig(P_o)
+//   c' = f c + i g            h' = o tanh(c')
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ void st4(float* p, const f32x4& v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void st4(bf16_t* p, const f32x4& v) {
+  *(bf16x4*)p = bf16x4{(bf16_t)v[0], (bf16_t)v[1], (bf16_t)v[2], (bf16_t)v[3]};
+}
+
+template <class S>
+__global__ void k_lpw_fwd(const float* __restrict__ P, const float* __restrict__ cprev,
+                          float* __restrict__ cout, S* __restrict__ hout, int npix, int ch) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= npix * 8) return;
+  const int pix = e >> 3, q = e & 7;
+  const float* pp = P + (size_t)pix * GC + 4 * q;
+  const f32x4 pi = ld4(pp), pf = ld4(pp + 32), pg = ld4(pp + 64), po = ld4(pp + 96);
+  f32x4 c = cprev ? ld4(cprev + (size_t)pix * HC + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 hn;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool live = 4 * q + j < ch;
+    const float cn = sigm(pf[j]) * c[j] + sigm(pi[j]) * ftanh(pg[j]);
+    c[j] = live ? cn : 0.f;
+    hn[j] = live ? sigm(po[j]) * ftanh(cn) : 0.f;
+  }
+  st4(cout + (size_t)pix * HC + 4 * q, c);
+  st4(hout + (size_t)pix * HC + 4 * q, hn);
+}
+
+// BPTT through one step.  dh: dL/dh_t (f32, CL), dc: dL/dc_t in, dL/dc_{t-1} out.
+//   tc = tanh c_t;  dc += dh o (1 - tc^2)
+//   dP_i = dc g i(1-i)   dP_f = dc c_{t-1} f(1-f)   dP_c = dc i (1-g^2)   dP_o = dh tc o(1-o)
+//   dc_{t-1} = dc f
+// dP -> dP_t (S) and dPsum (+=, f32; `first` initialises); `sum_s` gets an S
+// copy of the final dPsum (the last step of the sweep).
+template <class S>
+__global__ void k_lpw_bwd(const float* __restrict__ dh, float* __restrict__ dc,
+                          const float* __restrict__ P, const float* __restrict__ cc,
+                          const float* __restrict__ cprev, S* __restrict__ dP,
+                          float* __restrict__ dPsum, S* __restrict__ sum_s, int first, int npix,
+                          int ch) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= npix * 8) return;
+  const int pix = e >> 3, q = e & 7;
+  const size_t pg0 = (size_t)pix * GC + 4 * q, pc0 = (size_t)pix * HC + 4 * q;
+  const f32x4 pi = ld4(P + pg0), pf = ld4(P + pg0 + 32), pg = ld4(P + pg0 + 64),
+              po = ld4(P + pg0 + 96);
+  const f32x4 c = ld4(cc + pc0);
+  const f32x4 cp = cprev ? ld4(cprev + pc0) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 g_h = ld4(dh + pc0);
+  f32x4 g_c = ld4(dc + pc0);
+  f32x4 di, df, dg, dq, dcp;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool live = 4 * q + j < ch;
+    const float i = sigm(pi[j]), f = sigm(pf[j]), g = ftanh(pg[j]), o = sigm(po[j]);
+    const float tc = ftanh(c[j]);
+    const float dct = g_c[j] + g_h[j] * o * (1.f - tc * tc);
+    di[j] = live ? dct * g * i * (1.f - i) : 0.f;
+    df[j] = live ? dct * cp[j] * f * (1.f - f) : 0.f;
+    dg[j] = live ? dct * i * (1.f - g * g) : 0.f;
+    dq[j] = live ? g_h[j] * tc * o * (1.f - o) : 0.f;
+    dcp[j] = live ? dct * f : 0.f;
+  }
+  st4(dc + pc0, dcp);
+  st4(dP + pg0, di); st4(dP + pg0 + 32, df); st4(dP + pg0 + 64, dg); st4(dP + pg0 + 96, dq);
+  f32x4 s0 = di, s1 = df, s2 = dg, s3 = dq;
+  if (!first) {
+    s0 += ld4(dPsum + pg0); s1 += ld4(dPsum + pg0 + 32);
+    s2 += ld4(dPsum + pg0 + 64); s3 += ld4(dPsum + pg0 + 96);
+  }
+  st4(dPsum + pg0, s0); st4(dPsum + pg0 + 32, s1); st4(dPsum + pg0 + 64, s2); st4(dPsum + pg0 + 96, s3);
+  if (sum_s) {
+    st4(sum_s + pg0, s0); st4(sum_s + pg0 + 32, s1); st4(sum_s + pg0 + 64, s2); st4(sum_s + pg0 + 96, s3);
+  }
+}
+
+// Jacobian-penalty seeds at the last step (t = T-1), two VJPs per image:
+//   image b      : dh_t = 1, dc_t = 0   (J_h^T 1, through P_t only)
+//   image B + b  : dh_t = 0, dc_t = 1   (J_c^T 1, its h_{t-1} part)
+template <class S>
+__global__ void k_ljv_seed(const float* __restrict__ P, const float* __restrict__ cc,
+                           const float* __restrict__ cprev, S* __restrict__ dP, int npix, int ch) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= npix * 8) return;
+  const int pix = e >> 3, q = e & 7;
+  const size_t pg0 = (size_t)pix * GC + 4 * q, pc0 = (size_t)pix * HC + 4 * q;
+  const f32x4 pi = ld4(P + pg0), pf = ld4(P + pg0 + 32), pg = ld4(P + pg0 + 64),
+              po = ld4(P + pg0 + 96);
+  const f32x4 c = ld4(cc + pc0), cp = ld4(cprev + pc0);
+  f32x4 a0, a1, a2, a3, b0, b1, b2, b3;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool live = 4 * q + j < ch;
+    const float i = sigm(pi[j]), f = sigm(pf[j]), g = ftanh(pg[j]), o = sigm(po[j]);
+    const float tc = ftanh(c[j]);
+    const float dct = o * (1.f - tc * tc);            // seed dh = 1
+    a0[j] = live ? dct * g * i * (1.f - i) : 0.f;
+    a1[j] = live ? dct * cp[j] * f * (1.f - f) : 0.f;
+    a2[j] = live ? dct * i * (1.f - g * g) : 0.f;
+    a3[j] = live ? tc * o * (1.f - o) : 0.f;
+    b0[j] = live ? g * i * (1.f - i) : 0.f;           // seed dc = 1
+    b1[j] = live ? cp[j] * f * (1.f - f) : 0.f;
+    b2[j] = live ? i * (1.f - g * g) : 0.f;
+    b3[j] = 0.f;
+  }
+  S* d0 = dP + pg0;
+  S* d1 = dP + (size_t)npix * GC + pg0;
+  st4(d0, a0); st4(d0 + 32, a1); st4(d0 + 64, a2); st4(d0 + 96, a3);
+  st4(d1, b0); st4(d1 + 32, b1); st4(d1 + 64, b2); st4(d1 + 96, b3);
+}
+
+// jv = clamp(jh - mu)^2 + clamp(jc - mu)^2 with jh = conv^T part of seed 1 and
+// jc = f_{T-1} + dh'_{T-2} o_{T-2} (1 - tanh^2 c_{T-2})  -> NCHW fp32 [B][ch][NPIX]
+__global__ void k_ljv_final(const float* __restrict__ jdh, const float* __restrict__ Pl,
+                            const float* __restrict__ Pp, const float* __restrict__ cp, float mu,
+                            float* __restrict__ out, int B, int ch) {
+  const int n = B * NPIX * ch;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int pix = e % NPIX, c = (e / NPIX) % ch, b = e / (NPIX * ch);
+    const size_t p = (size_t)b * NPIX + pix;
+    const float jh = jdh[p * HC + c];
+    const float f = sigm(Pl[p * GC + 32 + c]);
+    const float o = sigm(Pp[p * GC + 96 + c]);
+    const float tc = ftanh(cp[p * HC + c]);
+    const float jc = f + jdh[((size_t)B * NPIX + p) * HC + c] * o * (1.f - tc * tc);
+    const float a = fmaxf(jh - mu, 0.f), bb = fmaxf(jc - mu, 0.f);
+    out[e] = a * a + bb * bb;
+  }
+}
+
+// ----------------------------------------------------------- weight grads
+// dW[g][co][ci][kh K + kw] = sum_{img, p} D_img[p][32 g + co] X_img[p + tap][ci]
+// over the image list (two segments, e.g. (h_{t-1}, dP_t) pairs).  Workgroup
+// (kh, slice): wave g owns gate g and the K taps of kernel row kh (K
+// accumulator tiles); D / X row bands are staged in LDS (double-buffered,
+// register prefetch), fragments come from ds_read_b64_tr_b16 transposed reads.
+template <class S> constexpr int lw_rb() { return sizeof(S) == 2 ? 4 : 2; }   // D rows per band
+template <class S, int K> struct LWBand {
+  static constexpr int P = K / 2;
+  static constexpr int TC = IMG + K - 1;
+  static constexpr int RBW = lw_rb<S>();
+  static constexpr int CPB = 16 / (int)sizeof(S);
+  static constexpr int XE = RBW * TC * HC;              // X band elements (with halo cols)
+  static constexpr int DE = RBW * IMG * GC;             // D band elements
+  static constexpr int BE = XE + DE;
+  static constexpr int XPER = RBW * IMG * (HC / CPB) / NT;   // 2
+  static constexpr int DPER = RBW * IMG * (GC / CPB) / NT;   // 8
+  static constexpr int BYTES = 2 * BE * (int)sizeof(S);
+  u32x4 x[XPER], d[DPER];
+  int xvalid;
+  __device__ __forceinline__ void load(const S* __restrict__ X, const S* __restrict__ D, int y0,
+                                       int kh, int tid) {
+    xvalid = 0;
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % (HC / CPB), pc = idx / (HC / CPB), col = pc % IMG, row = pc / IMG;
+      const int iy = y0 + row + kh - P;
+      const bool ok = iy >= 0 && iy < IMG;
+      x[j] = *(const u32x4*)(X + (size_t)((ok ? iy : 0) * IMG + col) * HC + q * CPB);
+      xvalid |= (int)ok << j;
+    }
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % (GC / CPB), pc = idx / (GC / CPB);
+      d[j] = *(const u32x4*)(D + (size_t)(y0 * IMG + pc) * GC + q * CPB);
+    }
+  }
+  __device__ __forceinline__ void store(S* xt, S* dt, int tid) const {
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % (HC / CPB), pc = idx / (HC / CPB), col = pc % IMG, row = pc / IMG;
+      *(u32x4*)(xt + (row * TC + col + P) * HC + q * CPB) =
+          (xvalid >> j) & 1 ? x[j] : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) {
+      const int idx = tid + j * NT;
+      *(u32x4*)(dt + idx * CPB) = d[j];
+    }
+  }
+};
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+__device__ __forceinline__ bf16x4 tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
+}
+template <int STRIDE>   // elements between pixel x and pixel x + 1
+__device__ __forceinline__ bf16x8 tr_read8(const bf16_t* p) {
+  return __builtin_shufflevector(tr_read(p), tr_read(p + 4 * STRIDE), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+struct LWgradArgs {
+  const void *X0, *D0, *X1, *D1;   // segment images: X [n][NPIX][32], D [n][NPIX][128] (S)
+  int n0, n1, nsl;
+  float* wslab;                     // [nsl][NG][K*K][32 co][32 ci]
+};
+
+template <class S, int K>
+__global__ __launch_bounds__(NT, 1) void k_lwgrad(LWgradArgs a) {
+  using Bd = LWBand<S, K>;
+  constexpr int KK = K * K, RBW = Bd::RBW, NBW = IMG / RBW, TC = Bd::TC;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  S* buf = (S*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);     // gate of this wave
+  const int kh = blockIdx.x, sl = blockIdx.y;
+  const int nimg = a.n0 + a.n1;
+  const int nmine = nimg > sl ? (nimg - sl + a.nsl - 1) / a.nsl : 0;
+  const int nunits = nmine * NBW;
+
+  f32x16 acc[K];
+#pragma unroll
+  for (int m = 0; m < K; ++m) acc[m] = zero16();
+  for (int i = tid; i < Bd::BYTES / 16; i += NT) ((u32x4*)buf)[i] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  auto unit_src = [&](int u, const S*& X, const S*& D, int& y0) {
+    const int j = sl + (u / NBW) * a.nsl;
+    y0 = (u % NBW) * RBW;
+    if (j < a.n0) {
+      X = (const S*)a.X0 + (size_t)j * NPIX * HC;
+      D = (const S*)a.D0 + (size_t)j * NPIX * GC;
+    } else {
+      X = (const S*)a.X1 + (size_t)(j - a.n0) * NPIX * HC;
+      D = (const S*)a.D1 + (size_t)(j - a.n0) * NPIX * GC;
+    }
+  };
+  Bd band;
+  if (nunits > 0) {
+    const S *X, *D;
+    int y0;
+    unit_src(0, X, D, y0);
+    band.load(X, D, y0, kh, tid);
+    band.store(buf, buf + Bd::XE, tid);
+  }
+  __syncthreads();
+  for (int u = 0; u < nunits; ++u) {
+    const S* xt = buf + (u & 1) * Bd::BE;
+    const S* dt = xt + Bd::XE;
+    const bool more = u + 1 < nunits;
+    if (more) {
+      const S *X, *D;
+      int y0;
+      unit_src(u + 1, X, D, y0);
+      band.load(X, D, y0, kh, tid);
+    }
+    if constexpr (sizeof(S) == 4) {
+      // k-step = 2 pixels (x0 + h); lane & 31 is ci for A (X), co for B (D)
+      const int c = lane & 31;
+      for (int yd = 0; yd < RBW; ++yd) {
+        const float* xb = (const float*)xt + (yd * TC + h) * HC + c;
+        const float* db = (const float*)dt + (yd * IMG + h) * GC + g * 32 + c;
+        for (int x0 = 0; x0 < IMG; x0 += 2) {
+          const float bv = db[x0 * GC];
+#pragma unroll
+          for (int m = 0; m < K; ++m) acc[m] = Tr<float>::mma(xb[(x0 + m) * HC], bv, acc[m]);
+        }
+      }
+    } else {
+      // k-step = 16 pixels; lane 4q+p' of each 16-lane group addresses pixel
+      // x0 + 8 hh + q (+4) and channels 16 (grp & 1) + 4 p' .. +3
+      const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
+      const int chb = 16 * (grp & 1) + 4 * pp, hh = grp >> 1;
+      constexpr int NSTEP = RBW * 2;
+      auto xaddr = [&](int st) {
+        const int yd = st >> 1, c0 = (st & 1) * 16 + 8 * hh + q;
+        return (const bf16_t*)xt + (yd * TC + c0) * HC + chb;
+      };
+      auto daddr = [&](int st) {
+        const int yd = st >> 1, c0 = (st & 1) * 16 + 8 * hh + q;
+        return (const bf16_t*)dt + (yd * IMG + c0) * GC + g * 32 + chb;
+      };
+      bf16x8 av[2][K], bv[2];
+      bv[0] = tr_read8<GC>(daddr(0));
+#pragma unroll
+      for (int m = 0; m < K; ++m) av[0][m] = tr_read8<HC>(xaddr(0) + m * HC);
+#pragma unroll
+      for (int st = 0; st < NSTEP; ++st) {
+        const int cur = st & 1, nxt = cur ^ 1;
+        if (st + 1 < NSTEP) {
+          bv[nxt] = tr_read8<GC>(daddr(st + 1));
+#pragma unroll
+          for (int m = 0; m < K; ++m) av[nxt][m] = tr_read8<HC>(xaddr(st + 1) + m * HC);
+        }
+#pragma unroll
+        for (int m = 0; m < K; ++m) acc[m] = Tr<bf16_t>::mma(av[cur][m], bv[cur], acc[m]);
+      }
+    }
+    if (more) {
+      S* xn = buf + ((u + 1) & 1) * Bd::BE;
+      band.store(xn, xn + Bd::XE, tid);
+      __syncthreads();
+    }
+  }
+  // acc[m]: rows ci = cl_x(r, h), cols co = lane & 31
+  float* dst = a.wslab + (((size_t)sl * NG + g) * KK + kh * K) * 1024;
+  const int co = lane & 31;
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[m * 1024 + co * 32 + cl_x(r, h)] = acc[m][r];
+  }
+}
+
+// ------------------------------------------------------------- reductions
+// Column sums of dPsum [npix][128] -> partial [nb][128] (bias gradients).
+__global__ void k_lcolsum(const float* __restrict__ src, float* __restrict__ part, int npix) {
+  const int c = threadIdx.x & 127, r0 = threadIdx.x >> 7;     // 256 threads: 2 row lanes
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int step = gridDim.x * 2;
+  int r = blockIdx.x * 2 + r0;
+  for (; r + 7 * step < npix; r += 8 * step) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += src[(size_t)(r + j * step) * GC + c];
+  }
+  for (; r < npix; r += step) s[0] += src[(size_t)r * GC + c];
+  float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __shared__ float red[256];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  if (threadIdx.x < 128) part[(size_t)blockIdx.x * GC + c] = red[c] + red[128 + c];
+}
+
+struct LReduceArgs {
+  int K, nsl_h, nsl_x, ch, cin, nb;
+  const float* wslab_h;   // [nsl_h][NG][KK][1024]
+  const float* wslab_x;   // [nsl_x][NG][KK][1024]
+  const float* colpart;   // [nb][128]
+  float* wh[4];
+  float* wx[4];
+  float* bx[4];
+};
+
+__device__ __forceinline__ float lsum(const float* __restrict__ p, size_t stride, int n) {
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += p[(size_t)(i + j) * stride];
+  }
+  for (; i < n; ++i) acc[0] += p[(size_t)i * stride];
+  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+__global__ void k_lreduce(LReduceArgs r) {
+  const int KK = r.K * r.K;
+  const int nw = NG * KK * 1024;
+  const int total = 2 * nw + GC;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    if (e < 2 * nw) {
+      const int fam = e / nw, rem = e % nw;            // 0: Wh, 1: Wx
+      const int g = rem / (KK * 1024), tap = (rem / 1024) % KK, co = (rem % 1024) / 32,
+                ci = rem % 32;
+      const int cin = fam == 0 ? r.ch : r.cin;
+      float* W = fam == 0 ? r.wh[g] : r.wx[g];
+      if (!W || co >= r.ch || ci >= cin) continue;
+      const float* src = fam == 0 ? r.wslab_h : r.wslab_x;
+      const int nsl = fam == 0 ? r.nsl_h : r.nsl_x;
+      W[((size_t)co * cin + ci) * KK + tap] = lsum(src + rem, (size_t)NG * KK * 1024, nsl);
+    } else {
+      const int c = e - 2 * nw, g = c / 32, co = c % 32;
+      if (r.bx[g] && co < r.ch) r.bx[g][co] = lsum(r.colpart + c, GC, r.nb);
+    }
+  }
+}
+
+// ------------------------------------------------------------ conversions
+// NCHW fp32 [B][nc][NPIX] -> channels-last [B][NPIX][32] (zero padded)
+template <class S>
+__global__ void k_to_cl(const float* __restrict__ src, S* __restrict__ dst, int B, int nc) {
+  const int n = B * NPIX * HC;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int c = e % HC, pix = (e / HC) % NPIX, b = e / (HC * NPIX);
+    dst[e] = (S)(c < nc ? src[((size_t)b * nc + c) * NPIX + pix] : 0.f);
+  }
+}
+template <class S>
+__global__ void k_from_cl(const S* __restrict__ src, float* __restrict__ dst, int B, int nc) {
+  const int n = B * nc * NPIX;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int pix = e % NPIX, c = (e / NPIX) % nc, b = e / (NPIX * nc);
+    dst[e] = ldf(src + ((size_t)b * NPIX + pix) * HC + c);
+  }
+}
+
+// ---------------------------------------------------------- parameter prep
+// fp32 torch weights -> MFMA A-operand fragments (weights on the A side):
+//   fwd  (NI = 1, NO = 4): F[o][0][tap][ks][lane][j]  = W_o[n = l&31][frag_chan(ks,h,j)][tap]
+//   conv^T (NI = 4, NO = 1): F[0][ig][tap][ks][lane][j] = W_ig[frag_chan][n = l&31][KK-1-tap]
+// (out-of-range channels are zero).  Families: 0 Wx fwd, 1 Wh fwd, 2 Wh^T, 3 Wx^T.
+struct LPrepArgs {
+  int K, ch, cin;
+  const float* wx[4];
+  const float* wh[4];
+  const float* bx[4];
+  void* fr[4];
+  float* bias;     // [128]
+};
+template <class S>
+__global__ void k_lprep(LPrepArgs p) {
+  using TT = Tr<S>;
+  const int KK = p.K * p.K;
+  const int per = NG * KK * TT::KS * 64 * TT::EPL;     // elements per family
+  const int total = 4 * per + GC;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    if (e >= 4 * per) {
+      const int c = e - 4 * per, g = c / 32, co = c % 32;
+      p.bias[c] = (p.bx[g] && co < p.ch) ? p.bx[g][co] : 0.f;
+      continue;
+    }
+    const int fam = e / per, r = e % per;
+    const int j = r % TT::EPL, l = (r / TT::EPL) % 64, ks = (r / (TT::EPL * 64)) % TT::KS;
+    const int tap = (r / (TT::EPL * 64 * TT::KS)) % KK, blk = r / (TT::EPL * 64 * TT::KS * KK);
+    const int n = l & 31, hh = l >> 5, kc = frag_chan<S>(ks, hh, j);
+    float v = 0.f;
+    if (fam < 2) {                      // blk = output gate o
+      const float* W = fam == 0 ? p.wx[blk] : p.wh[blk];
+      const int cin = fam == 0 ? p.cin : p.ch;
+      if (n < p.ch && kc < cin) v = W[((size_t)n * cin + kc) * KK + tap];
+    } else {                            // blk = input gate ig; out channel n = fwd input channel
+      const float* W = fam == 2 ? p.wh[blk] : p.wx[blk];
+      const int cin = fam == 2 ? p.ch : p.cin;
+      if (kc < p.ch && n < cin) v = W[((size_t)kc * cin + n) * KK + (KK - 1 - tap)];
+    }
+    ((S*)p.fr[fam])[r] = (S)v;
+  }
+}
+
+}  // namespace ptl
+
+// =========================================================================
+//                                  host side
+// =========================================================================
+using namespace ptl;
+
+static thread_local char g_err[512];
+static int fail(int code, const char* fmt, long v = 0) {
+  snprintf(g_err, sizeof(g_err), fmt, v);
+  return code;
+}
+
+namespace {
+
+constexpr size_t ALIGN = 256;
+inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
+
+struct LPlan {
+  int B, T, K, ch, cin, nsl_h, nsl_x, nb;
+  size_t es, npix;
+  // saved
+  size_t o_fr[4], o_bias, o_x, o_xg, o_h0, o_c0, o_P, o_h, o_c, saved;
+  // workspace
+  size_t o_dh, o_dc, o_dP, o_dPsum, o_dPsumS, o_jvP, o_wsh, o_wsx, o_col, ws;
+};
+
+int check(const pt_lstm_desc* d) {
+  if (!d) return fail(PT_LSTM_ERR_ARG, "null descriptor");
+  if (d->channels < 1 || d->channels > 32)
+    return fail(PT_LSTM_ERR_UNSUPPORTED, "hidden channels must be 1..32 (got %ld)", d->channels);
+  if (d->in_channels < 1 || d->in_channels > 32)
+    return fail(PT_LSTM_ERR_UNSUPPORTED, "input channels must be 1..32 (got %ld)", d->in_channels);
+  if (d->height != 32 || d->width != 32)
+    return fail(PT_LSTM_ERR_UNSUPPORTED, "only 32x32 images are supported (H=%ld)", d->height);
+  if (d->ksize < 1 || d->ksize > KMAX || (d->ksize & 1) == 0)
+    return fail(PT_LSTM_ERR_UNSUPPORTED, "ksize must be odd and <= 15 (got %ld)", d->ksize);
+  if (d->batch < 1 || d->steps < 1) return fail(PT_LSTM_ERR_ARG, "batch and steps must be >= 1%ld");
+  if (d->dtype != PT_LSTM_F32 && d->dtype != PT_LSTM_BF16) return fail(PT_LSTM_ERR_ARG, "bad dtype%ld");
+  return 0;
+}
+
+int slices(int nimg, int K) {
+  int n = (512 + K - 1) / K;           // ~512 workgroups over the K tap rows
+  if (n > nimg) n = nimg;
+  return n < 1 ? 1 : n;
+}
+
+LPlan plan(const pt_lstm_desc* d) {
+  LPlan p{};
+  p.B = d->batch; p.T = d->steps; p.K = d->ksize; p.ch = d->channels; p.cin = d->in_channels;
+  p.es = d->dtype == PT_LSTM_BF16 ? 2 : 4;
+  p.npix = (size_t)p.B * NPIX;
+  const size_t KK = (size_t)p.K * p.K;
+  size_t o = 0;
+  for (int i = 0; i < 4; ++i) { p.o_fr[i] = o; o += al(NG * KK * 1024 * p.es); }
+  p.o_bias = o; o += al(GC * 4);
+  p.o_x = o; o += al(p.npix * HC * p.es);
+  p.o_xg = o; o += al(p.npix * GC * 4);
+  p.o_h0 = o; o += al(p.npix * HC * p.es);
+  p.o_c0 = o; o += al(p.npix * HC * 4);
+  p.o_P = o; o += al(p.npix * GC * 4 * p.T);
+  p.o_h = o; o += al(p.npix * HC * p.es * p.T);
+  p.o_c = o; o += al(p.npix * HC * 4 * p.T);
+  p.saved = o;
+  p.nsl_h = slices(p.B * p.T, p.K);
+  p.nsl_x = slices(p.B, p.K);
+  p.nb = 256;
+  o = 0;
+  p.o_dh = o; o += al(2 * p.npix * HC * 4);
+  p.o_dc = o; o += al(p.npix * HC * 4);
+  p.o_dP = o; o += al(p.npix * GC * p.es * p.T);
+  p.o_dPsum = o; o += al(p.npix * GC * 4);
+  p.o_dPsumS = o; o += al(p.npix * GC * p.es);
+  p.o_jvP = o; o += al(2 * p.npix * GC * p.es);
+  p.o_wsh = o; o += al((size_t)p.nsl_h * NG * KK * 1024 * 4);
+  p.o_wsx = o; o += al((size_t)p.nsl_x * NG * KK * 1024 * 4);
+  p.o_col = o; o += al((size_t)p.nb * GC * 4);
+  p.ws = o;
+  return p;
+}
+
+#define HIPCHK(expr)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      snprintf(g_err, sizeof(g_err), "HIP error %s at line %d", hipGetErrorString(e_), __LINE__); \
+      return PT_LSTM_ERR_HIP;                                                            \
+    }                                                                                    \
+  } while (0)
+
+#define SETLDS(kern, bytes) \
+  HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
+
+// K dispatch (odd kernel sizes 1..15)
+#define K_SWITCH(K, CALL)                                  \
+  switch (K) {                                             \
+    case 1: { constexpr int KC = 1; CALL; } break;         \
+    case 3: { constexpr int KC = 3; CALL; } break;         \
+    case 5: { constexpr int KC = 5; CALL; } break;         \
+    case 7: { constexpr int KC = 7; CALL; } break;         \
+    case 9: { constexpr int KC = 9; CALL; } break;         \
+    case 11: { constexpr int KC = 11; CALL; } break;       \
+    case 13: { constexpr int KC = 13; CALL; } break;       \
+    default: { constexpr int KC = 15; CALL; } break;       \
+  }
+
+template <class S, int K, int NI, int NO>
+int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
+         hipStream_t st) {
+  using L = LTile<S, K>;
+  SETLDS((k_lconv<S, K, NI, NO>), L::BYTES);
+  LConvArgs a{src, wf, out, add, bias, nimg};
+  hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * NBAND), dim3(NT), L::BYTES, st, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+template <class S, int NI, int NO>
+int conv_k(int K, const void* src, const void* wf, float* out, const float* add, const float* bias,
+           int nimg, hipStream_t st) {
+  int rc = 0;
+  K_SWITCH(K, (rc = conv<S, KC, NI, NO>(src, wf, out, add, bias, nimg, st)));
+  return rc;
+}
+
+template <class S, int K>
+int wgrad(const LWgradArgs& a, hipStream_t st) {
+  using Bd = LWBand<S, K>;
+  SETLDS((k_lwgrad<S, K>), Bd::BYTES);
+  hipLaunchKernelGGL((k_lwgrad<S, K>), dim3(K, a.nsl), dim3(NT), Bd::BYTES, st, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+template <class S>
+int wgrad_k(int K, const LWgradArgs& a, hipStream_t st) {
+  int rc = 0;
+  K_SWITCH(K, (rc = wgrad<S, KC>(a, st)));
+  return rc;
+}
+
+inline dim3 grid_for(size_t n, int bs = 256) {
+  size_t g = (n + bs - 1) / bs;
+  return dim3((unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g)));
+}
+
+template <class S>
+int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr, const float* h0,
+                const float* c0, char* sv, float* h_out, float* c_out, hipStream_t st) {
+  const LPlan p = plan(d);
+  const int npix = (int)p.npix;
+  LPrepArgs pa{};
+  pa.K = p.K; pa.ch = p.ch; pa.cin = p.cin;
+  for (int g = 0; g < 4; ++g) {
+    if (!pr->wx[g] || !pr->wh[g]) return fail(PT_LSTM_ERR_ARG, "missing gate weight %ld", g);
+    pa.wx[g] = pr->wx[g]; pa.wh[g] = pr->wh[g]; pa.bx[g] = pr->bx[g];
+  }
+  for (int i = 0; i < 4; ++i) pa.fr[i] = sv + p.o_fr[i];
+  pa.bias = (float*)(sv + p.o_bias);
+  hipLaunchKernelGGL(k_lprep<S>, dim3(1024), dim3(256), 0, st, pa);
+  HIPCHK(hipGetLastError());
+
+  S* xcl = (S*)(sv + p.o_x);
+  hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, x, xcl, p.B, p.cin);
+  S* hinit = h0 ? (S*)(sv + p.o_h0) : nullptr;
+  float* cinit = c0 ? (float*)(sv + p.o_c0) : nullptr;
+  if (h0) hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, h0, hinit, p.B, p.ch);
+  if (c0) hipLaunchKernelGGL(k_to_cl<float>, grid_for(p.npix * HC), dim3(256), 0, st, c0, cinit, p.B, p.ch);
+  HIPCHK(hipGetLastError());
+
+  float* P = (float*)(sv + p.o_P);
+  S* H = (S*)(sv + p.o_h);
+  float* Cc = (float*)(sv + p.o_c);
+  const size_t pstep = p.npix * GC, hstep = p.npix * HC;
+  float* xg = h0 ? (float*)(sv + p.o_xg) : P;      // without h0, P_0 = xg
+  if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], xg, nullptr, pa.bias, p.B, st)) return rc;
+  for (int t = 0; t < p.T; ++t) {
+    const S* hin = t == 0 ? hinit : H + (t - 1) * hstep;
+    if (hin)
+      if (int rc = conv_k<S, 1, 4>(p.K, hin, sv + p.o_fr[1], P + t * pstep, xg, nullptr, p.B, st))
+        return rc;
+    const float* cprev = t == 0 ? cinit : Cc + (t - 1) * hstep;
+    hipLaunchKernelGGL(k_lpw_fwd<S>, grid_for((size_t)npix * 8), dim3(256), 0, st,
+                       (const float*)(P + t * pstep), cprev, Cc + t * hstep, H + t * hstep, npix, p.ch);
+    HIPCHK(hipGetLastError());
+  }
+  if (h_out)
+    hipLaunchKernelGGL(k_from_cl<S>, grid_for(p.npix * p.ch), dim3(256), 0, st,
+                       (const S*)(H + (p.T - 1) * hstep), h_out, p.B, p.ch);
+  if (c_out)
+    hipLaunchKernelGGL(k_from_cl<float>, grid_for(p.npix * p.ch), dim3(256), 0, st,
+                       (const float*)(Cc + (p.T - 1) * hstep), c_out, p.B, p.ch);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+template <class S>
+int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
+                 const float* d_h, const float* d_c, const pt_lstm_grads* g, int has_h0,
+                 int has_c0, hipStream_t st) {
+  const LPlan p = plan(d);
+  const int npix = (int)p.npix;
+  const size_t pstep = p.npix * GC, hstep = p.npix * HC;
+  const float* P = (const float*)(sv + p.o_P);
+  const S* H = (const S*)(sv + p.o_h);
+  const float* Cc = (const float*)(sv + p.o_c);
+  const float* cinit = has_c0 ? (const float*)(sv + p.o_c0) : nullptr;
+  float* dh = (float*)(ws + p.o_dh);
+  float* dc = (float*)(ws + p.o_dc);
+  S* dP = (S*)(ws + p.o_dP);
+  float* dPsum = (float*)(ws + p.o_dPsum);
+  S* dPsumS = (S*)(ws + p.o_dPsumS);
+
+  hipLaunchKernelGGL(k_to_cl<float>, grid_for(p.npix * HC), dim3(256), 0, st, d_h, dh, p.B, p.ch);
+  if (d_c)
+    hipLaunchKernelGGL(k_to_cl<float>, grid_for(p.npix * HC), dim3(256), 0, st, d_c, dc, p.B, p.ch);
+  else
+    HIPCHK(hipMemsetAsync(dc, 0, p.npix * HC * 4, st));
+  HIPCHK(hipGetLastError());
+  const bool want_dh0 = has_h0 && g->d_h0;
+  for (int t = p.T - 1; t >= 0; --t) {
+    const float* cprev = t == 0 ? cinit : Cc + (t - 1) * hstep;
+    hipLaunchKernelGGL(k_lpw_bwd<S>, grid_for((size_t)npix * 8), dim3(256), 0, st, (const float*)dh,
+                       dc, P + t * pstep, Cc + t * hstep, cprev, dP + t * pstep, dPsum,
+                       t == 0 ? dPsumS : (S*)nullptr, (int)(t == p.T - 1), npix, p.ch);
+    HIPCHK(hipGetLastError());
+    if (t > 0 || want_dh0)
+      if (int rc = conv_k<S, 4, 1>(p.K, dP + t * pstep, sv + p.o_fr[2], dh, nullptr, nullptr, p.B, st))
+        return rc;
+  }
+  if (want_dh0)
+    hipLaunchKernelGGL(k_from_cl<float>, grid_for(p.npix * p.ch), dim3(256), 0, st,
+                       (const float*)dh, g->d_h0, p.B, p.ch);
+  if (has_c0 && g->d_c0)
+    hipLaunchKernelGGL(k_from_cl<float>, grid_for(p.npix * p.ch), dim3(256), 0, st,
+                       (const float*)dc, g->d_c0, p.B, p.ch);
+  HIPCHK(hipGetLastError());
+
+  // weight gradients: Wh over (h_{t-1}, dP_t), t >= 1 (+ (h0, dP_0)); Wx over (x, sum_t dP_t)
+  LWgradArgs wa{};
+  wa.X0 = H; wa.D0 = dP + pstep; wa.n0 = p.B * (p.T - 1);
+  wa.X1 = sv + p.o_h0; wa.D1 = dP; wa.n1 = has_h0 ? p.B : 0;
+  wa.nsl = p.nsl_h;
+  wa.wslab = (float*)(ws + p.o_wsh);
+  if (int rc = wgrad_k<S>(p.K, wa, st)) return rc;
+  LWgradArgs wx{};
+  wx.X0 = sv + p.o_x; wx.D0 = dPsumS; wx.n0 = p.B;
+  wx.X1 = nullptr; wx.D1 = nullptr; wx.n1 = 0;
+  wx.nsl = p.nsl_x;
+  wx.wslab = (float*)(ws + p.o_wsx);
+  if (int rc = wgrad_k<S>(p.K, wx, st)) return rc;
+  float* colp = (float*)(ws + p.o_col);
+  hipLaunchKernelGGL(k_lcolsum, dim3(p.nb), dim3(256), 0, st, (const float*)dPsum, colp, npix);
+  LReduceArgs ra{};
+  ra.K = p.K; ra.nsl_h = p.nsl_h; ra.nsl_x = p.nsl_x; ra.ch = p.ch; ra.cin = p.cin; ra.nb = p.nb;
+  ra.wslab_h = wa.wslab; ra.wslab_x = wx.wslab; ra.colpart = colp;
+  for (int i = 0; i < 4; ++i) { ra.wh[i] = g->wh[i]; ra.wx[i] = g->wx[i]; ra.bx[i] = g->bx[i]; }
+  hipLaunchKernelGGL(k_lreduce, dim3(1024), dim3(256), 0, st, ra);
+  HIPCHK(hipGetLastError());
+  if (g->d_x) {
+    if (int rc = conv_k<S, 4, 1>(p.K, dPsumS, sv + p.o_fr[3], dh, nullptr, nullptr, p.B, st)) return rc;
+    hipLaunchKernelGGL(k_from_cl<float>, grid_for(p.npix * p.cin), dim3(256), 0, st,
+                       (const float*)dh, g->d_x, p.B, p.cin);
+    HIPCHK(hipGetLastError());
+  }
+  return 0;
+}
+
+template <class S>
+int run_jv(const pt_lstm_desc* d, const char* sv, char* ws, float mu, float* jv, hipStream_t st) {
+  const LPlan p = plan(d);
+  const int npix = (int)p.npix;
+  const size_t pstep = p.npix * GC, hstep = p.npix * HC;
+  const float* P = (const float*)(sv + p.o_P);
+  const float* Cc = (const float*)(sv + p.o_c);
+  S* jP = (S*)(ws + p.o_jvP);
+  float* jdh = (float*)(ws + p.o_dh);
+  const int t = p.T - 1;
+  hipLaunchKernelGGL(k_ljv_seed<S>, grid_for((size_t)npix * 8), dim3(256), 0, st, P + t * pstep,
+                     Cc + t * hstep, Cc + (t - 1) * hstep, jP, npix, p.ch);
+  HIPCHK(hipGetLastError());
+  if (int rc = conv_k<S, 4, 1>(p.K, jP, sv + p.o_fr[2], jdh, nullptr, nullptr, 2 * p.B, st)) return rc;
+  hipLaunchKernelGGL(k_ljv_final, grid_for(p.npix * p.ch), dim3(256), 0, st, (const float*)jdh,
+                     P + t * pstep, P + (t - 1) * pstep, Cc + (t - 1) * hstep, mu, jv, p.B, p.ch);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pt_lstm_saved_bytes(const pt_lstm_desc* d) {
+  if (check(d)) return 0;
+  return plan(d).saved;
+}
+size_t pt_lstm_workspace_bytes(const pt_lstm_desc* d) {
+  if (check(d)) return 0;
+  return plan(d).ws;
+}
+
+int pt_lstm_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* p,
+                    const float* h0, const float* c0, void* saved, float* h_out, float* c_out,
+                    pt_lstm_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  if (!x || !p || !saved) return fail(PT_LSTM_ERR_ARG, "null x / params / saved%ld");
+  if (!!h0 != !!(d->init_state & PT_LSTM_H0) || !!c0 != !!(d->init_state & PT_LSTM_C0))
+    return fail(PT_LSTM_ERR_ARG, "h0 / c0 do not match desc.init_state (%ld)", d->init_state);
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == PT_LSTM_BF16
+             ? run_forward<bf16_t>(d, x, p, h0, c0, (char*)saved, h_out, c_out, st)
+             : run_forward<float>(d, x, p, h0, c0, (char*)saved, h_out, c_out, st);
+}
+
+int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace, const float* d_h,
+                     const float* d_c, const pt_lstm_grads* g, pt_lstm_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  if (!saved || !workspace || !d_h || !g) return fail(PT_LSTM_ERR_ARG, "null saved / workspace / d_h / grads%ld");
+  hipStream_t st = (hipStream_t)stream;
+  const int hh = (d->init_state & PT_LSTM_H0) != 0, hc = (d->init_state & PT_LSTM_C0) != 0;
+  return d->dtype == PT_LSTM_BF16
+             ? run_backward<bf16_t>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, hh, hc, st)
+             : run_backward<float>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, hh, hc, st);
+}
+
+int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace, float mu,
+                       float* jv, pt_lstm_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  if (d->steps < 2)
+    return fail(PT_LSTM_ERR_ARG, "the Jacobian penalty needs steps >= 2 (got %ld)", d->steps);
+  if (!saved || !workspace || !jv) return fail(PT_LSTM_ERR_ARG, "null saved / workspace / jv%ld");
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == PT_LSTM_BF16
+             ? run_jv<bf16_t>(d, (const char*)saved, (char*)workspace, mu, jv, st)
+             : run_jv<float>(d, (const char*)saved, (char*)workspace, mu, jv, st);
+}
+
+const char* pt_lstm_last_error(void) { return g_err; }
+const char* pt_lstm_version(void) { return "pt_lstm 0.1 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,193 @@
+"""ConvLSTM — drop-in for the reference ``models/convlstm.py`` on MI355X.
+
+Same class names, constructor signatures, ``forward`` signatures / return
+tuples and ``state_dict`` keys as the reference (``dummyhgru`` :9-54,
+``ConvLSTMCell`` :57-90, ``ConvLSTM`` :93-166), and the same parameter
+initialisation in the same RNG order (conv0 is registered, then overwritten
+by the Gabor bank, :103-106; conv6 gets xavier-normal weights and a
+log(99) bias, :112-114).
+
+The recurrence runs in the HIP library ``libptlstm.so`` (include/pt_lstm.h)
+through ``ptamd.lstm.LSTMStepsFn``: with ``grad_method='bptt'`` the whole
+``timesteps``-step loop (:137-143) and its BPTT are two library calls, and
+the training-mode Jacobian penalty (:150-161) a third.  conv0 + pow (:118-119),
+BN (:146), conv6 (:147) and the criterion stay in PyTorch.  The cell-level
+``ConvLSTMCell.forward(x, h, c)`` is one library step with given states, so
+``grad_method='rbp'`` (:124-135, Neumann-series backward in ``dummyhgru``)
+works unchanged on top of it.
+
+Differences from the reference, by design: ``jv_penalty`` is returned without
+a graph even when ``jacobian_penalty=True`` (the reference never adds it to the
+returned loss; differentiating it would need a double backward through the
+fused cell, which raises); the image must be 32x32 and ``filt_size`` odd <= 15.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.autograd import Function
+from torch.nn import init
+
+from ptamd.lstm import run_steps
+
+_DEFAULT_DTYPE = os.environ.get("PT_CELL_DTYPE", "f32")
+_GABOR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "utils",
+                      "gabor_serre.npy")
+
+
+class dummyhgru(Function):
+    """Neumann-series recurrent back-propagation (reference models/convlstm.py:9-54).
+
+    Forward passes ``last_state`` through; backward replaces its gradient by
+    sum_k (J^T)^k g, J = d last_state / d state_2nd_last, truncated at
+    ``truncate_iter`` terms or as soon as the series stops contracting
+    (norm > 1, a growing term, or a vanishing one).
+    """
+
+    @staticmethod
+    def forward(ctx, state_2nd_last, last_state, *args):
+        ctx.save_for_backward(state_2nd_last, last_state)
+        ctx.args = args
+        return last_state
+
+    @staticmethod
+    def backward(ctx, grad):
+        state_2nd_last, last_state = ctx.saved_tensors
+        truncate_iter = ctx.args[-1]
+        g_prev = grad.clone()
+        v_prev = grad.clone()
+        norm_v = [torch.norm(g_prev).item()]
+        g = g_prev
+        for _ in range(truncate_iter):
+            v = torch.autograd.grad(last_state, state_2nd_last, grad_outputs=v_prev,
+                                    retain_graph=True, allow_unused=True)[0]
+            nv = torch.norm(v)
+            g = g_prev + v
+            ng = torch.norm(g)
+            if ng > 1 or nv > norm_v[-1] or nv < 1e-9:
+                g = g_prev
+                break
+            v_prev, g_prev = v, g
+            norm_v.append(nv.item())
+        return (None, g, None, None, None, None)
+
+
+class ConvLSTMCell(nn.Module):
+    """ConvLSTM cell parameters and one step (reference models/convlstm.py:57-90).
+
+    x-convs carry a bias, h-convs do not; peephole weights Wci/Wcf/Wco are None
+    as in the reference.  ``forward(x, h, c)`` runs one step on the device.
+    """
+
+    def __init__(self, input_channels, hidden_channels, kernel_size):
+        super().__init__()
+        self.input_channels = input_channels
+        self.hidden_channels = hidden_channels
+        self.kernel_size = kernel_size
+        self.num_features = 4
+        self.padding = int((kernel_size - 1) / 2)
+        for g in ("i", "f", "c", "o"):
+            setattr(self, f"Wx{g}", nn.Conv2d(self.input_channels, self.hidden_channels,
+                                               self.kernel_size, 1, self.padding, bias=True))
+            setattr(self, f"Wh{g}", nn.Conv2d(self.hidden_channels, self.hidden_channels,
+                                               self.kernel_size, 1, self.padding, bias=False))
+        self.Wci = None
+        self.Wcf = None
+        self.Wco = None
+        self.cell_dtype = _DEFAULT_DTYPE
+
+    def cell_weights(self):
+        """[Wx_i..o, bx_i..o, Wh_i..o] in the order ptamd.lstm expects."""
+        gs = ("i", "f", "c", "o")
+        return ([getattr(self, f"Wx{g}").weight for g in gs]
+                + [getattr(self, f"Wx{g}").bias for g in gs]
+                + [getattr(self, f"Wh{g}").weight for g in gs])
+
+    def steps(self, x, timesteps, h=None, c=None, want_jv=False, mu=0.9):
+        """``timesteps`` steps from (h, c) (None = zeros): (h_T, c_T, jv)."""
+        return run_steps(x, self.cell_weights(), ksize=self.kernel_size, steps=timesteps,
+                         h0=h, c0=c, dtype=self.cell_dtype, want_jv=want_jv, mu=mu)
+
+    def forward(self, x, h, c):
+        h_t, c_t, _ = self.steps(x, 1, h, c)
+        return h_t, c_t
+
+
+class ConvLSTM(nn.Module):
+    """Reference models/convlstm.py:93-166 (static-image ConvLSTM, 25 channels)."""
+
+    def __init__(self, timesteps=8, filt_size=15, num_iter=50, exp_name='exp1',
+                 jacobian_penalty=False, grad_method='bptt'):
+        super().__init__()
+        self.timesteps = timesteps
+        self.num_iter = num_iter
+        self.exp_name = exp_name
+        self.jacobian_penalty = jacobian_penalty
+        self.grad_method = grad_method
+        self.conv0 = nn.Conv2d(1, 25, kernel_size=7, padding=3)
+        part1 = np.load(_GABOR, allow_pickle=False)
+        self.conv0.weight.data = torch.FloatTensor(part1)
+        self.unit1 = ConvLSTMCell(25, 25, filt_size)
+        print("Training with filter size:", filt_size, "x", filt_size)
+        self.bn = nn.BatchNorm2d(25, eps=1e-03, track_running_stats=False)
+        self.conv6 = nn.Conv2d(25, 2, kernel_size=1)
+        init.xavier_normal_(self.conv6.weight)
+        init.constant_(self.conv6.bias, torch.log(torch.tensor((1 - 0.01) / 0.01)))
+
+    @property
+    def cell_dtype(self):
+        return self.unit1.cell_dtype
+
+    @cell_dtype.setter
+    def cell_dtype(self, v):
+        self.unit1.cell_dtype = v
+
+    def forward(self, x, epoch, itr, target, criterion, testmode=False):
+        x = self.conv0(x)
+        x = torch.pow(x, 2)
+        states = []
+        jv_penalty = None
+        if self.grad_method == 'rbp':
+            internal_h = torch.zeros_like(x)
+            internal_c = torch.zeros_like(x)
+            with torch.no_grad():
+                for _ in range(self.timesteps - 1):
+                    if testmode:
+                        states.append(internal_h)
+                    internal_h, internal_c = self.unit1(x, internal_h, internal_c)
+            if testmode:
+                states.append(internal_h)
+            state_2nd_last = internal_h.detach().requires_grad_()
+            state_2nd_last_c = internal_c.detach().requires_grad_()
+            last_state, internal_c = self.unit1(x, state_2nd_last, state_2nd_last_c)
+            internal_h = dummyhgru.apply(state_2nd_last, last_state, epoch, itr, self.exp_name,
+                                         self.num_iter)
+            if testmode:
+                states.append(internal_h)
+            if self.training:
+                ones = torch.ones_like(last_state)
+                jv = torch.autograd.grad(last_state, state_2nd_last, grad_outputs=[ones],
+                                         retain_graph=True, allow_unused=True)[0]
+                jv_penalty = (jv - 0.90).clamp(0) ** 2
+                jv = torch.autograd.grad(internal_c, state_2nd_last_c, grad_outputs=[ones],
+                                         retain_graph=True, allow_unused=True)[0]
+                jv_penalty = jv_penalty + (jv - 0.90).clamp(0) ** 2
+        elif self.grad_method == 'bptt':
+            if self.training and self.timesteps < 2:
+                raise RuntimeError("ConvLSTM training needs timesteps >= 2 (the reference's "
+                                   "state_2nd_last is unbound otherwise, convlstm.py:140-161)")
+            internal_h, _, jv = self.unit1.steps(x, self.timesteps, want_jv=self.training)
+            if self.training:
+                jv_penalty = jv
+        else:
+            raise ValueError(f"unknown grad_method {self.grad_method!r}")
+
+        output = self.bn(internal_h)
+        output = self.conv6(output)
+        loss = criterion(output, target)
+        if jv_penalty is None:
+            jv_penalty = torch.tensor([1]).float().to(output.device)
+        if testmode:
+            return output, states, loss
+        return output, jv_penalty, loss

@@ -1,7 +1,9 @@
-"""Build the HIP extension in-tree for gfx950: ``python -m ptamd.build``.
+"""Build the HIP extensions in-tree for gfx950: ``python -m ptamd.build``.
 
-One ``hipcc -shared -fPIC`` line; the resulting ``libptcell.so`` sits next to
-``_lib.py`` so it travels with the repository snapshot to the GPU box.
+One ``hipcc -shared -fPIC`` line per library (run in parallel); the resulting
+``libptcell.so`` (InT / hGRU cell, include/pt_cell.h) and ``libptlstm.so``
+(ConvLSTM cell, include/pt_lstm.h) sit next to the ctypes bindings so they
+travel with the repository snapshot to the GPU box.
 """
 from __future__ import annotations
 
@@ -13,28 +15,51 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-OUT = os.path.join(HERE, "libptcell.so")
-SOURCES = [os.path.join(CSRC, "pt_cell.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, "pt_device.h"), os.path.join(REPO, "include", "pt_cell.h")]
+INC = os.path.join(REPO, "include")
+
+# library -> (sources, extra dependencies)
+LIBS = {
+    "libptcell.so": ([os.path.join(CSRC, "pt_cell.hip")],
+                     [os.path.join(CSRC, "pt_device.h"), os.path.join(INC, "pt_cell.h")]),
+    "libptlstm.so": ([os.path.join(CSRC, "pt_lstm.hip")],
+                     [os.path.join(CSRC, "pt_device.h"), os.path.join(INC, "pt_lstm.h")]),
+}
+OUT = os.path.join(HERE, "libptcell.so")      # kept for callers of the old single-library API
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(OUT):
+def _out(lib: str) -> str:
+    return os.path.join(HERE, lib)
+
+
+def up_to_date(lib: str = "libptcell.so") -> bool:
+    out = _out(lib)
+    if not os.path.exists(out):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
+    t = os.path.getmtime(out)
+    srcs, deps = LIBS[lib]
+    return all(os.path.getmtime(d) <= t for d in srcs + deps)
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
-        return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(REPO, "include"), "-o", OUT + ".tmp", *SOURCES]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    procs = []
+    for lib, (srcs, _) in LIBS.items():
+        if not force and up_to_date(lib):
+            continue
+        out = _out(lib)
+        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-I", INC, "-o", out + ".tmp", *srcs]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((lib, out, subprocess.Popen(cmd)))
+    failed = []
+    for lib, out, p in procs:
+        if p.wait() != 0:
+            failed.append(lib)
+        else:
+            os.replace(out + ".tmp", out)
+    if failed:
+        raise RuntimeError(f"hipcc failed for {', '.join(failed)}")
     return OUT
 
 

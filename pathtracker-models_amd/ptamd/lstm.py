@@ -1,0 +1,211 @@
+"""ctypes binding of ``libptlstm.so`` (include/pt_lstm.h) and its autograd bridge.
+
+``LSTMStepsFn`` runs ``steps`` ConvLSTM steps on a static input through the
+HIP library — forward, BPTT backward and (for the model's training mode) the
+Jacobian penalty — with every buffer owned by torch and the library seeing raw
+device pointers plus the current HIP stream.  It replaces, for the reference's
+``models/convlstm.py``, the per-step Python loop (:137-143, cell :84-90) and
+autograd through it.  There is no CPU fallback: CPU tensors or a missing
+library raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+from torch.autograd.function import once_differentiable
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libptlstm.so")
+
+PT_LSTM_F32, PT_LSTM_BF16 = 0, 1
+PT_LSTM_H0, PT_LSTM_C0 = 1, 2
+
+# Exported symbols declared in include/pt_lstm.h (tests check all are present).
+EXPORTS = ("pt_lstm_saved_bytes", "pt_lstm_workspace_bytes", "pt_lstm_forward",
+           "pt_lstm_backward", "pt_lstm_jv_penalty", "pt_lstm_last_error", "pt_lstm_version")
+
+_P = ctypes.c_void_p
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("in_channels", ctypes.c_int32),
+                ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("ksize", ctypes.c_int32),
+                ("steps", ctypes.c_int32), ("dtype", ctypes.c_int32),
+                ("init_state", ctypes.c_int32)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("wx", _P * 4), ("bx", _P * 4), ("wh", _P * 4)]
+
+
+class Grads(ctypes.Structure):
+    _fields_ = [("wx", _P * 4), ("bx", _P * 4), ("wh", _P * 4), ("d_x", _P), ("d_h0", _P),
+                ("d_c0", _P)]
+
+
+class PtLstmError(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load():
+    """Load (once) and return the library; raise if it is not built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise PtLstmError(
+                f"{LIB_PATH} is missing: build the HIP extensions first "
+                "(python __graft_entry__.py build, or python -m ptamd.build)")
+        lib = ctypes.CDLL(LIB_PATH)
+        D = ctypes.POINTER(Desc)
+        lib.pt_lstm_saved_bytes.restype = ctypes.c_size_t
+        lib.pt_lstm_saved_bytes.argtypes = [D]
+        lib.pt_lstm_workspace_bytes.restype = ctypes.c_size_t
+        lib.pt_lstm_workspace_bytes.argtypes = [D]
+        lib.pt_lstm_forward.restype = ctypes.c_int
+        lib.pt_lstm_forward.argtypes = [D, _P, ctypes.POINTER(Params), _P, _P, _P, _P, _P, _P]
+        lib.pt_lstm_backward.restype = ctypes.c_int
+        lib.pt_lstm_backward.argtypes = [D, _P, _P, _P, _P, ctypes.POINTER(Grads), _P]
+        lib.pt_lstm_jv_penalty.restype = ctypes.c_int
+        lib.pt_lstm_jv_penalty.argtypes = [D, _P, _P, ctypes.c_float, _P, _P]
+        lib.pt_lstm_last_error.restype = ctypes.c_char_p
+        lib.pt_lstm_version.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().pt_lstm_last_error().decode(errors="replace")
+        raise PtLstmError(f"pt_lstm error {rc}: {msg}")
+
+
+DTYPES = {"f32": PT_LSTM_F32, "fp32": PT_LSTM_F32, "float32": PT_LSTM_F32,
+          "bf16": PT_LSTM_BF16, "bfloat16": PT_LSTM_BF16}
+
+
+def make_desc(x, channels: int, ksize: int, steps: int, dtype: str, h0=None, c0=None) -> Desc:
+    b, cin, h, w = x.shape
+    return Desc(batch=b, in_channels=cin, channels=channels, height=h, width=w, ksize=ksize,
+                steps=steps, dtype=DTYPES[dtype],
+                init_state=(PT_LSTM_H0 if h0 is not None else 0)
+                | (PT_LSTM_C0 if c0 is not None else 0))
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_device(x):
+    if x.device.type != "cuda":
+        raise RuntimeError("the ConvLSTM HIP cell runs on a ROCm device only (got a "
+                           f"{x.device.type} tensor); there is no CPU fallback")
+
+
+# weight order handed to the Function: Wx{i,f,c,o}, bx{i,f,c,o}, Wh{i,f,c,o}
+GATES = ("i", "f", "c", "o")
+
+
+class LSTMStepsFn(torch.autograd.Function):
+    """(x, h0|None, c0|None, 12 weights) -> (h_T, c_T, jv).
+
+    ``jv`` (the training-mode Jacobian penalty, models/convlstm.py:150-161) is
+    only computed when ``want_jv``; it is returned detached (the reference
+    builds a graph for it only with ``jacobian_penalty=True``, and never puts
+    it in the loss it returns).
+    """
+
+    @staticmethod
+    def forward(ctx, x, h0, c0, ksize: int, steps: int, dtype: str, want_jv: bool, mu: float,
+                *weights):
+        _require_device(x)
+        lib = load()
+        x = x.contiguous().float()
+        h0 = h0.contiguous().float() if h0 is not None else None
+        c0 = c0.contiguous().float() if c0 is not None else None
+        weights = [w.contiguous().float() for w in weights]
+        ch = weights[0].shape[0]
+        d = make_desc(x, ch, ksize, steps, dtype, h0, c0)
+        nsaved = lib.pt_lstm_saved_bytes(ctypes.byref(d))
+        if nsaved == 0:
+            check(1)
+        saved = torch.empty(nsaved, dtype=torch.uint8, device=x.device)
+        b, _, hh, ww = x.shape
+        h_out = torch.empty((b, ch, hh, ww), dtype=torch.float32, device=x.device)
+        c_out = torch.empty_like(h_out)
+        pp = Params()
+        for g in range(4):
+            pp.wx[g] = weights[g].data_ptr()
+            pp.bx[g] = weights[4 + g].data_ptr()
+            pp.wh[g] = weights[8 + g].data_ptr()
+        st = _stream(x.device)
+        check(lib.pt_lstm_forward(ctypes.byref(d), _ptr(x), ctypes.byref(pp), _ptr(h0), _ptr(c0),
+                                  _ptr(saved), _ptr(h_out), _ptr(c_out), st))
+        jv = torch.empty((0,), device=x.device)
+        if want_jv:
+            ws = torch.empty(lib.pt_lstm_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                             device=x.device)
+            jv = torch.empty_like(h_out)
+            check(lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
+                                         _ptr(jv), st))
+        ctx.meta = (ksize, steps, dtype, h0 is not None, c0 is not None, tuple(x.shape), ch)
+        ctx.saved_blob = saved
+        ctx.wshapes = [w.shape for w in weights]
+        ctx.mark_non_differentiable(jv)
+        return h_out, c_out, jv
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, d_h, d_c, _d_jv):
+        # may run several times on one graph (retain_graph: the rbp Neumann
+        # series and the Jacobian-penalty VJPs, models/convlstm.py:35,155-160),
+        # so the saved blob stays with ctx until autograd frees the graph
+        lib = load()
+        ksize, steps, dtype, has_h0, has_c0, xshape, ch = ctx.meta
+        b, cin, hh, ww = xshape
+        dev = ctx.saved_blob.device
+        d = Desc(batch=b, in_channels=cin, channels=ch, height=hh, width=ww, ksize=ksize,
+                 steps=steps, dtype=DTYPES[dtype],
+                 init_state=(PT_LSTM_H0 if has_h0 else 0) | (PT_LSTM_C0 if has_c0 else 0))
+        if d_h is None:
+            d_h = torch.zeros((b, ch, hh, ww), device=dev)
+        d_h = d_h.contiguous().float()
+        d_c = d_c.contiguous().float() if d_c is not None else None
+        ws = torch.empty(lib.pt_lstm_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                         device=dev)
+        need = ctx.needs_input_grad
+        grads = [torch.empty(s, device=dev) if need[8 + i] else None
+                 for i, s in enumerate(ctx.wshapes)]
+        dx = torch.empty(xshape, device=dev) if need[0] else None
+        dh0 = torch.empty((b, ch, hh, ww), device=dev) if (has_h0 and need[1]) else None
+        dc0 = torch.empty((b, ch, hh, ww), device=dev) if (has_c0 and need[2]) else None
+        gg = Grads()
+        for g in range(4):
+            gg.wx[g] = grads[g].data_ptr() if grads[g] is not None else 0
+            gg.bx[g] = grads[4 + g].data_ptr() if grads[4 + g] is not None else 0
+            gg.wh[g] = grads[8 + g].data_ptr() if grads[8 + g] is not None else 0
+        gg.d_x = dx.data_ptr() if dx is not None else 0
+        gg.d_h0 = dh0.data_ptr() if dh0 is not None else 0
+        gg.d_c0 = dc0.data_ptr() if dc0 is not None else 0
+        check(lib.pt_lstm_backward(ctypes.byref(d), _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_h),
+                                   _ptr(d_c), ctypes.byref(gg), _stream(dev)))
+        return (dx, dh0, dc0, None, None, None, None, None, *grads)
+
+
+def run_steps(x, weights, *, ksize: int, steps: int, h0=None, c0=None, dtype: str = "f32",
+              want_jv: bool = False, mu: float = 0.9):
+    """Apply ``steps`` ConvLSTM steps.  ``weights``: [Wx_i..o, bx_i..o, Wh_i..o]."""
+    return LSTMStepsFn.apply(x, h0, c0, ksize, steps, dtype, want_jv, mu, *weights)

@@ -204,6 +204,21 @@ def make_init_hgru(ref_hgru, tag, seed=123):
     print(tag, len(sd), "tensors")
 
 
+def make_init_convlstm(ref_clstm, tag, seed=123, filt=7):
+    """ConvLSTM initial parameters under a fixed seed (conv0 overwritten by the
+    Gabor bank, conv6 xavier-normal; convlstm.py:103-114)."""
+    torch.manual_seed(seed)
+    cwd = os.getcwd()
+    os.chdir(REF)
+    try:
+        model = ref_clstm.ConvLSTM(timesteps=4, filt_size=filt)
+    finally:
+        os.chdir(cwd)
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **sd)
+    print(tag, len(sd), "tensors")
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not mounted; golden vectors are generated in the build container only")
@@ -234,6 +249,7 @@ def main():
             "hgru_c32": lambda: make_hgru(ref_hgru, "hgru_c32", batch=2, t_len=6, dims=32, seed=6),
             "hgru_b4t16": lambda: make_hgru(ref_hgru, "hgru_b4t16", batch=4, t_len=16, dims=32,
                                             seed=8, want_gates=False),
+            "init_convlstm_seed123": lambda: make_init_convlstm(ref_clstm, "init_convlstm_seed123"),
             "convlstm_k7": lambda: make_convlstm(ref_clstm, "convlstm_k7", batch=2, timesteps=4,
                                                  filt=7, seed=7),
             # the reference default filt_size=15 (convlstm.py:95) and the shortest

@@ -19,22 +19,28 @@ from goldens import GOLDEN, load
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _header_symbols():
-    txt = open(os.path.join(REPO, "include", "pt_cell.h")).read()
+def _header_symbols(header="pt_cell.h"):
+    txt = open(os.path.join(REPO, "include", header)).read()
     return sorted(set(re.findall(r"\b(pt_[a-z_]+)\s*\(", txt)))
 
 
+def _bindings():
+    from ptamd import _lib, lstm
+    return [("pt_cell.h", _lib, "pt_version", "pt_cell"),
+            ("pt_lstm.h", lstm, "pt_lstm_version", "pt_lstm")]
+
+
 def test_header_and_binding_agree():
-    from ptamd import _lib
-    assert sorted(_lib.EXPORTS) == _header_symbols()
+    for header, mod, _, _ in _bindings():
+        assert sorted(mod.EXPORTS) == _header_symbols(header), header
 
 
 def test_library_exports_every_symbol():
-    from ptamd import _lib
-    lib = _lib.load()
-    for sym in _header_symbols():
-        assert hasattr(lib, sym), sym
-    assert lib.pt_version().decode().startswith("pt_cell")
+    for header, mod, ver, prefix in _bindings():
+        lib = mod.load()
+        for sym in _header_symbols(header):
+            assert hasattr(lib, sym), (header, sym)
+        assert getattr(lib, ver)().decode().startswith(prefix)
 
 
 def test_size_queries_and_validation():
@@ -107,3 +113,46 @@ def test_no_cpu_fallback():
     m = int_mod.InT(dimensions=32, timesteps=4, kernel_size=7)
     with pytest.raises(RuntimeError, match="ROCm device"):
         m(torch.rand(1, 3, 4, 32, 32))
+
+
+def test_lstm_size_queries_and_validation():
+    from ptamd import lstm
+    lib = lstm.load()
+    d = lstm.Desc(batch=256, in_channels=25, channels=25, height=32, width=32, ksize=15,
+                  steps=8, dtype=lstm.PT_LSTM_BF16, init_state=0)
+    saved = lib.pt_lstm_saved_bytes(ctypes.byref(d))
+    step = 256 * 1024
+    assert saved >= 8 * step * (128 * 4 + 32 * 2 + 32 * 4)   # P_t, h_t, c_t per step
+    assert lib.pt_lstm_workspace_bytes(ctypes.byref(d)) >= 8 * step * 128 * 2
+    for field, val, msg in (("ksize", 4, b"ksize"), ("ksize", 17, b"ksize"),
+                            ("channels", 33, b"hidden"), ("height", 64, b"32x32"),
+                            ("steps", 0, b"steps")):
+        bad = lstm.Desc(batch=2, in_channels=25, channels=25, height=32, width=32, ksize=7,
+                        steps=4, dtype=0, init_state=0)
+        setattr(bad, field, val)
+        assert lib.pt_lstm_saved_bytes(ctypes.byref(bad)) == 0, field
+        assert msg in lib.pt_lstm_last_error(), (field, lib.pt_lstm_last_error())
+
+
+def test_convlstm_keys_and_init_match_reference():
+    """ConvLSTM drop-in: state_dict keys in the reference order (convlstm.py:93-114)
+    and initial values under seed 123 bit-identical (Gabor conv0, RNG order)."""
+    from models import convlstm as cl
+    z = np.load(os.path.join(GOLDEN, "init_convlstm_seed123.npz"), allow_pickle=False)
+    torch.manual_seed(123)
+    m = cl.ConvLSTM(timesteps=4, filt_size=7)
+    sd = m.state_dict()
+    assert list(sd) == list(z.files)
+    for k in z.files:
+        np.testing.assert_array_equal(sd[k].numpy(), z[k], err_msg=k)
+    g = np.load(os.path.join(GOLDEN, "convlstm_k15.npz"), allow_pickle=False)
+    m15 = cl.ConvLSTM(timesteps=3, filt_size=15)
+    assert list(m15.state_dict()) == [k[len("param."):] for k in g.files if k.startswith("param.")]
+
+
+def test_convlstm_no_cpu_fallback():
+    from models import convlstm as cl
+    m = cl.ConvLSTM(timesteps=2, filt_size=7)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        m(torch.rand(1, 1, 32, 32), 0, 0, torch.zeros(1, 32, 32, dtype=torch.long),
+          torch.nn.CrossEntropyLoss())
