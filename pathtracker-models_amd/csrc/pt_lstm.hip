@@ -21,9 +21,10 @@
 //   x_cl  [B][1024][32] S         xg, P_t [B][1024][128] f32 (gate g at 32 g)
 //   h_t   [T][B][1024][32] S      c_t     [T][B][1024][32] f32
 //   dP_t  [T][B][1024][128] S     dPsum   [B][1024][128] f32 (+ an S copy)
-// Conv kernels tile the 32x32 image in 4 bands of 8 output rows; the band plus
-// its (k-1)-row / (k-1)-column zero halo is one LDS tile (22 x 46 x 32 bf16 =
-// 63 KB at k = 15).
+// The forward conv tiles the 32x32 image in 4 bands of 8 output rows; the band
+// plus its (k-1)-row / (k-1)-column zero halo is one LDS tile (22 x 46 x 32
+// bf16 = 63 KB at k = 15).  The transposed conv takes the whole image per
+// workgroup (46 x 46 x 32 bf16 = 132 KB at k = 15).
 #include "pt_device.h"
 #include "../../include/pt_lstm.h"
 
@@ -37,12 +38,15 @@ using namespace ptc;
 constexpr int HC = 32;             // padded hidden / input channels
 constexpr int NG = 4;              // gates i, f, c, o
 constexpr int GC = NG * HC;        // 128
-constexpr int RB = 8;              // output rows per conv band
-constexpr int NBAND = IMG / RB;    // 4
 constexpr int KMAX = 15;
+// output rows per conv workgroup: 8 for the 4-gate forward (one gate tile per
+// wave, 8 rows each), the whole image for the 4-gates-in transposed conv (one
+// output tile: each wave takes 8 rows, so both variants reuse every LDS
+// fragment across up to 8 output rows)
+template <int NO> constexpr int conv_rb() { return NO == 4 ? 8 : IMG; }
 
 // ------------------------------------------------------------------ conv tile
-template <class S, int K> struct LTile {
+template <class S, int K, int RB> struct LTile {
   static constexpr int P = K / 2;
   static constexpr int TR = RB + K - 1;      // tile rows
   static constexpr int TC = IMG + K - 1;     // tile columns
@@ -79,10 +83,11 @@ template <class S, int K, int NI, int NO>
 __global__ __launch_bounds__(NT, 1) void k_lconv(LConvArgs a) {
   using TT = Tr<S>;
   using F = typename TT::frag;
-  using L = LTile<S, K>;
+  constexpr int RB = conv_rb<NO>(), NBAND = IMG / RB;
+  using L = LTile<S, K, RB>;
   constexpr int KK = K * K;
   constexpr int KSP = TT::KS / TT::NPASS;
-  constexpr int RW = RB * NO / NWAVE;        // 8 (NO = 4) or 2 (NO = 1)
+  constexpr int RW = RB * NO / NWAVE;        // 8
   constexpr int NTR = RW + K - 1;
   constexpr int CPB = 16 / (int)sizeof(S);   // channels per 16-B chunk
   constexpr int NCH = L::CP / CPB;           // chunks per pixel per pass (4)
@@ -729,10 +734,11 @@ LPlan plan(const pt_lstm_desc* d) {
 template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
          hipStream_t st) {
-  using L = LTile<S, K>;
+  using L = LTile<S, K, conv_rb<NO>()>;
   SETLDS((k_lconv<S, K, NI, NO>), L::BYTES);
   LConvArgs a{src, wf, out, add, bias, nimg};
-  hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * NBAND), dim3(NT), L::BYTES, st, a);
+  hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(NT),
+                     L::BYTES, st, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
