@@ -17,6 +17,7 @@
 // partial sums (fp64 atomics), the next kernel finalises them (kernel boundary
 // = grid-wide sync).  See DESIGN.md §3.
 #include "pt_device.h"
+#include "pt_graph.h"
 #include "../../include/pt_cell.h"
 
 #include <stdio.h>
@@ -1546,6 +1547,17 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   return 0;
 }
 
+// Whole forward / backward launch sequences replayed as hipGraphs (pt_graph.h);
+// off while kernel timing is enabled (that pass wants per-launch events).
+ptg::GraphCache g_graphs;
+bool use_graph() {
+  return ptg::graphs_enabled() && __atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) == 0;
+}
+int ablate_env() {
+  const char* ab = getenv("PT_CELL_ABLATE");
+  return ab ? atoi(ab) : 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1563,9 +1575,17 @@ int pt_cell_forward(const pt_cell_desc* d, const float* x, const pt_cell_params*
                     void* ws, float* e_last, float* gates, pt_stream_t stream) {
   if (int rc = check(d)) return rc;
   if (!x || !p || !saved || !ws) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
-  if (d->dtype == PT_DTYPE_BF16)
-    return run_forward<bf16_t>(d, x, p, saved, ws, e_last, gates, (hipStream_t)stream);
-  return run_forward<float>(d, x, p, saved, ws, e_last, gates, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  const bool bf = d->dtype == PT_DTYPE_BF16;
+  auto body = [&](hipStream_t s) {
+    return bf ? run_forward<bf16_t>(d, x, p, saved, ws, e_last, gates, s)
+              : run_forward<float>(d, x, p, saved, ws, e_last, gates, s);
+  };
+  if (!use_graph()) return body(st);
+  if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
+  ptg::Key k;
+  k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env());
+  return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 
 int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, pt_stream_t stream) {
@@ -1589,9 +1609,17 @@ int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params
                      pt_stream_t stream) {
   if (int rc = check(d)) return rc;
   if (!x || !p || !saved || !ws || !d_e_last || !g) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
-  if (d->dtype == PT_DTYPE_BF16)
-    return run_backward<bf16_t>(d, x, p, saved, ws, d_e_last, g, (hipStream_t)stream);
-  return run_backward<float>(d, x, p, saved, ws, d_e_last, g, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  const bool bf = d->dtype == PT_DTYPE_BF16;
+  auto body = [&](hipStream_t s) {
+    return bf ? run_backward<bf16_t>(d, x, p, saved, ws, d_e_last, g, s)
+              : run_backward<float>(d, x, p, saved, ws, d_e_last, g, s);
+  };
+  if (!use_graph()) return body(st);
+  if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
+  ptg::Key k;
+  k.add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env());
+  return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 
 int pt_cell_timing_enable(uint32_t kind_mask) {

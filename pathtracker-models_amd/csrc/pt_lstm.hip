@@ -26,6 +26,7 @@
 // bf16 = 63 KB at k = 15).  The transposed conv takes the whole image per
 // workgroup (46 x 46 x 32 bf16 = 132 KB at k = 15).
 #include "pt_device.h"
+#include "pt_graph.h"
 #include "../../include/pt_lstm.h"
 
 #include <stdio.h>
@@ -735,7 +736,6 @@ template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
          hipStream_t st) {
   using L = LTile<S, K, conv_rb<NO>()>;
-  SETLDS((k_lconv<S, K, NI, NO>), L::BYTES);
   LConvArgs a{src, wf, out, add, bias, nimg};
   hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(NT),
                      L::BYTES, st, a);
@@ -754,7 +754,6 @@ int conv_k(int K, const void* src, const void* wf, float* out, const float* add,
 template <class S, int K>
 int wgrad(const LWgradArgs& a, hipStream_t st) {
   using Bd = LWBand<S, K>;
-  SETLDS((k_lwgrad<S, K>), Bd::BYTES);
   hipLaunchKernelGGL((k_lwgrad<S, K>), dim3(K, a.nsl), dim3(NT), Bd::BYTES, st, a);
   HIPCHK(hipGetLastError());
   return 0;
@@ -766,6 +765,27 @@ int wgrad_k(int K, const LWgradArgs& a, hipStream_t st) {
   K_SWITCH(K, (rc = wgrad<S, KC>(a, st)));
   return rc;
 }
+
+// dynamic-LDS limits of the K-specific kernels, set once per (S, K) outside
+// any stream capture
+template <class S, int K>
+int prime_k() {
+  static bool done = false;     // idempotent; a race only repeats the calls
+  if (done) return 0;
+  SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<4>()>::BYTES));
+  SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<1>()>::BYTES));
+  SETLDS((k_lwgrad<S, K>), (LWBand<S, K>::BYTES));
+  done = true;
+  return 0;
+}
+template <class S>
+int prime(int K) {
+  int rc = 0;
+  K_SWITCH(K, (rc = prime_k<S, KC>()));
+  return rc;
+}
+
+ptg::GraphCache g_graphs;
 
 inline dim3 grid_for(size_t n, int bs = 256) {
   size_t g = (n + bs - 1) / bs;
@@ -934,21 +954,35 @@ int pt_lstm_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params*
   if (!x || !p || !saved) return fail(PT_LSTM_ERR_ARG, "null x / params / saved%ld");
   if (!!h0 != !!(d->init_state & PT_LSTM_H0) || !!c0 != !!(d->init_state & PT_LSTM_C0))
     return fail(PT_LSTM_ERR_ARG, "h0 / c0 do not match desc.init_state (%ld)", d->init_state);
+  const bool bf = d->dtype == PT_LSTM_BF16;
+  if (int rc = bf ? prime<bf16_t>(d->ksize) : prime<float>(d->ksize)) return rc;
+  auto body = [&](hipStream_t s) {
+    return bf ? run_forward<bf16_t>(d, x, p, h0, c0, (char*)saved, h_out, c_out, s)
+              : run_forward<float>(d, x, p, h0, c0, (char*)saved, h_out, c_out, s);
+  };
   hipStream_t st = (hipStream_t)stream;
-  return d->dtype == PT_LSTM_BF16
-             ? run_forward<bf16_t>(d, x, p, h0, c0, (char*)saved, h_out, c_out, st)
-             : run_forward<float>(d, x, p, h0, c0, (char*)saved, h_out, c_out, st);
+  if (!ptg::graphs_enabled()) return body(st);
+  ptg::Key k;
+  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out);
+  return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
 int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace, const float* d_h,
                      const float* d_c, const pt_lstm_grads* g, pt_lstm_stream_t stream) {
   if (int rc = check(d)) return rc;
   if (!saved || !workspace || !d_h || !g) return fail(PT_LSTM_ERR_ARG, "null saved / workspace / d_h / grads%ld");
-  hipStream_t st = (hipStream_t)stream;
   const int hh = (d->init_state & PT_LSTM_H0) != 0, hc = (d->init_state & PT_LSTM_C0) != 0;
-  return d->dtype == PT_LSTM_BF16
-             ? run_backward<bf16_t>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, hh, hc, st)
-             : run_backward<float>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, hh, hc, st);
+  const bool bf = d->dtype == PT_LSTM_BF16;
+  if (int rc = bf ? prime<bf16_t>(d->ksize) : prime<float>(d->ksize)) return rc;
+  auto body = [&](hipStream_t s) {
+    return bf ? run_backward<bf16_t>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, hh, hc, s)
+              : run_backward<float>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, hh, hc, s);
+  };
+  hipStream_t st = (hipStream_t)stream;
+  if (!ptg::graphs_enabled()) return body(st);
+  ptg::Key k;
+  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g);
+  return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
 int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace, float mu,
@@ -957,10 +991,11 @@ int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace
   if (d->steps < 2)
     return fail(PT_LSTM_ERR_ARG, "the Jacobian penalty needs steps >= 2 (got %ld)", d->steps);
   if (!saved || !workspace || !jv) return fail(PT_LSTM_ERR_ARG, "null saved / workspace / jv%ld");
+  const bool bf = d->dtype == PT_LSTM_BF16;
+  if (int rc = bf ? prime<bf16_t>(d->ksize) : prime<float>(d->ksize)) return rc;
   hipStream_t st = (hipStream_t)stream;
-  return d->dtype == PT_LSTM_BF16
-             ? run_jv<bf16_t>(d, (const char*)saved, (char*)workspace, mu, jv, st)
-             : run_jv<float>(d, (const char*)saved, (char*)workspace, mu, jv, st);
+  return bf ? run_jv<bf16_t>(d, (const char*)saved, (char*)workspace, mu, jv, st)
+            : run_jv<float>(d, (const char*)saved, (char*)workspace, mu, jv, st);
 }
 
 const char* pt_lstm_last_error(void) { return g_err; }

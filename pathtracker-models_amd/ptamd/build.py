@@ -20,9 +20,11 @@ INC = os.path.join(REPO, "include")
 # library -> (sources, extra dependencies)
 LIBS = {
     "libptcell.so": ([os.path.join(CSRC, "pt_cell.hip")],
-                     [os.path.join(CSRC, "pt_device.h"), os.path.join(INC, "pt_cell.h")]),
+                     [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
+                      os.path.join(INC, "pt_cell.h")]),
     "libptlstm.so": ([os.path.join(CSRC, "pt_lstm.hip")],
-                     [os.path.join(CSRC, "pt_device.h"), os.path.join(INC, "pt_lstm.h")]),
+                     [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
+                      os.path.join(INC, "pt_lstm.h")]),
 }
 OUT = os.path.join(HERE, "libptcell.so")      # kept for callers of the old single-library API
 
