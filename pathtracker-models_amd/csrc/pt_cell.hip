@@ -38,6 +38,11 @@ enum SmallSlot {
 constexpr int SLAB_G = 6 * 1024;                 // 6 gate weights [n][ci]
 constexpr int SLAB = SLAB_G + NSMALL * 32;
 constexpr int NTRANS = 12;                       // backward transients incl. dAt, GEfin
+// BatchNorm batch sums are fp64 atomics spread over NBNC copies (workgroup w
+// adds into copy w % NBNC; readers sum the copies): with one copy, all 256-1024
+// workgroups of a launch serialised on the same 64-96 addresses (measured
+// 7.5 us per forward conv launch, 5 us per k_pw_bb launch).
+constexpr int NBNC = 16;
 
 // ----------------------------------------------------------------- arguments
 template <class S>
@@ -62,14 +67,14 @@ struct CellArgs {
   S *E, *I, *gE, *ci, *ce, *eg;         // saved per frame [T][B][32][32][32]
   S* at;                                // hGRU only: attention map per frame (the gated inhibition)
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
-  double* bnacc;                        // fwd BN sums [T][2][3][32]: sum mean_b, sum mean_b^2, sum M2_b
+  double* bnacc;                        // fwd BN sums [T][2][NBNC][3][32]: sum mean_b, sum mean_b^2, sum M2_b
   float* gates;                         // [B][T][C][32][32] or null
   // backward transients, channels-last [B][32][32][32] in the storage type
   S *dEn, *dcE, *dIl, *dEp, *dcI, *GI, *dgEp, *dxp, *dgE, *dIt;
   S* dAt;                               // hGRU: d loss / d att_t through the gated inhibition
   const float* GEfin;                   // dE of the last frame (channels-last)
   S *dci_s, *dce_s;                     // [T][B][32][32][32] conv-output grads (for k_wgrad)
-  double* bnbacc;                       // bwd BN sums [T][2][2][32]: sum dy, sum dy*xhat
+  double* bnbacc;                       // bwd BN sums [T][2][NBNC][2][32]: sum dy, sum dy*xhat
   float* slab;                          // [B][PW_PARTS][SLAB]
   int conv_done;                        // k_pw_ba: dgE holds conv^T(w_inh) + dgEp
 };
@@ -109,7 +114,11 @@ __device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const St
 __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps, float* stat,
                                 float* gstat, int tid) {
   if (tid < 32) {
-    const double s1 = acc[tid], s2 = acc[32 + tid], s3 = acc[64 + tid];
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NBNC; ++k) {
+      s1 += acc[k * 96 + tid]; s2 += acc[k * 96 + 32 + tid]; s3 += acc[k * 96 + 64 + tid];
+    }
     const double mean = s1 / B;
     double m2 = s3 + (double)NPIX * (s2 - s1 * s1 / B);
     m2 = m2 > 0.0 ? m2 : 0.0;
@@ -157,6 +166,7 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) { sm += red[w * 32 + tid]; v += red[128 + w * 32 + tid]; }
     const double mn = (double)(sm * (1.f / NPIX));
+    out += (blockIdx.x % NBNC) * 96;
     unsafeAtomicAdd(out + tid, mn);
     unsafeAtomicAdd(out + 32 + tid, mn * mn);
     unsafeAtomicAdd(out + 64 + tid, (double)v);
@@ -216,7 +226,10 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
     if (tid < 32) {
       // dx = A dy + Bc raw + Cc  with A = rstd g, xhat = (raw - mean) rstd
       const double inv = 1.0 / ((double)a.B * NPIX);
-      const float md = (float)(a.bnb[tid] * inv), mdx = (float)(a.bnb[32 + tid] * inv);
+      double sd = 0.0, sdx = 0.0;
+#pragma unroll
+      for (int k = 0; k < NBNC; ++k) { sd += a.bnb[k * 64 + tid]; sdx += a.bnb[k * 64 + 32 + tid]; }
+      const float md = (float)(sd * inv), mdx = (float)(sdx * inv);
       const float mean = a.bnstat[tid], rstd = a.bnstat[32 + tid];
       const float A = rstd * a.bnw[tid];
       tbl[tid] = A;
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
         store_pl(a.out_raw + cb + ((size_t)(wave * RPW + i) * IMG + px) * C, h, acc[i]);
-      bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
+      if (!(a.ablate & 8)) bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
     } else {
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
@@ -306,12 +319,17 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
 constexpr int PW_NT = 512;
 constexpr int PW_NW = PW_NT / 64;
 constexpr int PWF_RPP = 1;                         // forward rows per wave
-constexpr int PWA_RPP = 2;                         // k_pw_ba rows per wave
+// k_pw_ba takes a whole clip per workgroup (4 rows per wave, in a loop): its
+// fixed per-workgroup cost (slab prefetch / flush, x staging, LDS clears,
+// reductions) is paid once per clip (measured 59.3 -> 56.8 us per launch).
+// k_pw_bb stays at one row per wave: looping its body spills (~46 VGPRs) and
+// doubled its row cost.
+constexpr int PWA_RPP = 4;                         // k_pw_ba rows per wave
 constexpr int PWB_RPP = 1;                         // k_pw_bb rows per wave (register bound)
 constexpr int PWF_WGPC = IMG / (PW_NW * PWF_RPP);  // workgroups per clip (4)
-constexpr int PWA_WGPC = IMG / (PW_NW * PWA_RPP);  // (2)
+constexpr int PWA_WGPC = IMG / (PW_NW * PWA_RPP);  // (1)
 constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (4)
-constexpr int PW_PARTS = PWB_WGPC;                 // slab partitions per clip (>= PWA_WGPC)
+constexpr int PW_PARTS = PWB_WGPC > PWA_WGPC ? PWB_WGPC : PWA_WGPC;   // slab partitions per clip
 
 constexpr int PW_NGACC = 4;   // 1x1 weight-gradient tiles accumulated in LDS per workgroup
 template <int RPP, bool BWD>
@@ -369,16 +387,24 @@ __device__ __forceinline__ void gacc_row(float* gacc_g, float* flush, const f32x
 __device__ void gacc_zero(float* g, int n, int tid) {
   for (int e = tid; e < n * 1024; e += PW_NT) g[e] = 0.f;
 }
-// The workgroup's slab partition is copied into LDS by LDS-DMA at kernel
-// start (its latency hides under the staging loads); the flushes at the end
-// then store old + new without waiting on a global read-modify-write.
-__device__ __forceinline__ void slab_prefetch(const float* slab_p, float* slabl, int wave, int lane) {
-  constexpr int NCHUNK = SLAB / 4;                       // 16-B chunks
-  for (int j = wave; j * 64 < NCHUNK; j += PW_NW)
-    if (j * 64 + lane < NCHUNK)
-      __builtin_amdgcn_global_load_lds((const void*)(slab_p + (j * 64 + lane) * 4),
-                                       (__attribute__((address_space(3))) void*)(slabl + j * 256),
+// The workgroup's slab fields are copied into LDS by LDS-DMA at kernel start
+// (their latency hides under the staging loads); the flushes at the end then
+// store old + new without waiting on a global read-modify-write.  Only the
+// fields this kernel updates are fetched: gate-weight tiles [g0, g0 + ng) and
+// the per-channel block.
+__device__ __forceinline__ void slab_range(const float* slab_p, float* slabl, int f0, int nf,
+                                           int wave, int lane) {
+  const int nchunk = nf / 4;                             // 16-B chunks
+  for (int j = wave; j * 64 < nchunk; j += PW_NW)
+    if (j * 64 + lane < nchunk)
+      __builtin_amdgcn_global_load_lds((const void*)(slab_p + f0 + (j * 64 + lane) * 4),
+                                       (__attribute__((address_space(3))) void*)(slabl + f0 + j * 256),
                                        16, 0, 0);
+}
+__device__ __forceinline__ void slab_prefetch(const float* slab_p, float* slabl, int g0, int ng,
+                                              int wave, int lane) {
+  slab_range(slab_p, slabl, g0 * 1024, ng * 1024, wave, lane);
+  slab_range(slab_p, slabl, SLAB_G, NSMALL * 32, wave, lane);
 }
 // slab[g0 + k] = slab copy + gacc[k] for k < n (after a barrier)
 __device__ void gacc_flush(const float* g, const float* slabl, float* slab_p, int g0, int n, int tid) {
@@ -421,6 +447,7 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int 
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int w = 0; w < PW_NW; ++w) { a += red[w * 32 + tid]; b += red[256 + w * 32 + tid]; }
+    out += (blockIdx.x % NBNC) * 64;
     unsafeAtomicAdd(out + tid, (double)a);
     unsafeAtomicAdd(out + 32 + tid, (double)b);
   }
@@ -460,7 +487,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   }
   if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
   if (t > 0)
-    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * 96, B, a.eps, L.stat + 64,
+    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
@@ -555,7 +582,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   if constexpr (HG) gi = load_pk(a.at + t * fs + ro, c, h);
   else gi = Iv;
   stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
-  bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * 96, B, a.eps, L.stat,
+  bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, B, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
@@ -613,7 +640,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   const bool tail = tt <= T - 1, head = t >= 0;
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
-  slab_prefetch(slab_p, L.slabl, wave, lane);
+  slab_prefetch(slab_p, L.slabl, 0, 2, wave, lane);        // a_w, a_u
   if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWA_RPP, tid, PW_NT);
   gacc_zero(L.gacc, 2, tid);
   __syncthreads();
@@ -714,7 +741,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
-  if (head && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * 64, lane, wave, tid);
+  if (head && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64, lane, wave, tid);
   if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
   if (tail && (head || HG) && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
 }
@@ -762,7 +789,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
     dIt = load_pk(a.dIt + ro, c, h);
     civ = load_pk(a.ci + t * fs + ro, c, h);
   }
-  slab_prefetch(slab_p, L.slabl, wave, lane);
+  slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);        // i_w, i_u, e_w, e_u
   stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
   gacc_zero(L.gacc, 4, tid);
   __syncthreads();
@@ -859,7 +886,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   }
   sm[4] = bs1;
   sm[5] = bs0;
-  if (!a.no_inh && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * 64, lane, wave, tid);
+  if (!a.no_inh && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64, lane, wave, tid);
   if (a.ablate & 32) return;
   flush_small<6>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5
@@ -1324,8 +1351,8 @@ Plan plan(const pt_cell_desc* d) {
   for (int i = 0; i < 12; ++i) { p.o_g[i] = o; o += al((size_t)C * C * p.es); }
   p.saved = o;
   o = 0;
-  p.o_bnacc = o; o += al((size_t)p.T * 2 * 96 * 8);
-  p.o_bnbacc = o; o += al((size_t)p.T * 2 * 64 * 8);
+  p.o_bnacc = o; o += al((size_t)p.T * 2 * NBNC * 96 * 8);
+  p.o_bnbacc = o; o += al((size_t)p.T * 2 * NBNC * 64 * 8);
   for (int i = 0; i < NTRANS; ++i) { p.o_tr[i] = o; o += al(p.frame * 4); }   // GEfin f32
   p.o_dci = o; o += fbytes;
   p.o_dce = o; o += fbytes;
@@ -1448,7 +1475,7 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   }
   pa.wf_inh = (S*)((char*)saved + p.o_wf[0]); pa.wf_exc = (S*)((char*)saved + p.o_wf[1]);
   pa.wt_inh = (S*)((char*)saved + p.o_wf[2]); pa.wt_exc = (S*)((char*)saved + p.o_wf[3]);
-  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnacc, 0, (size_t)p.T * 2 * 96 * 8, st));
+  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnacc, 0, (size_t)p.T * 2 * NBNC * 96 * 8, st));
   timed(PT_K_PREP, st, [&] { hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa); });
   const dim3 gpf(p.B * PWF_WGPC);
   const size_t lpf = (pw_lds_bytes<PWF_RPP, false>()), lcv = conv_lds_bytes<S>();
@@ -1461,12 +1488,12 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
     timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });
     if (t == p.T) break;
     if (!d->no_inh) {
-      ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * 96;
+      ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96;
       timed(PT_K_CONV_FA, st, [&] {
         hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, ca); });
     }
     timed(PT_K_PW_FB, st, [&] { PW_LAUNCH(k_pw_fb, gpf, lpf); });
-    cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * 96;
+    cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * NBNC * 96;
     timed(PT_K_CONV_FB, st, [&] {
       hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, cb); });
   }
@@ -1486,7 +1513,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
   HIPCHK(hipMemsetAsync((char*)ws + p.o_slab, 0, (size_t)p.B * PW_PARTS * SLAB * 4, st));
-  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnbacc, 0, (size_t)p.T * 2 * 64 * 8, st));
+  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnbacc, 0, (size_t)p.T * 2 * NBNC * 64 * 8, st));
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
@@ -1501,7 +1528,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
     cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
-    cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
+    cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
     cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
     timed(PT_K_CONV_BB, st, [&] {
       hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_ADD>), dim3(p.B), dim3(NT), lcv, st, cb); });
@@ -1512,7 +1539,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
       // dgE_t = conv^T(BN0-bwd(dcI), w_inh) + e_u^T d_e_pre ; frame 0's conv^T is dead (E_{-1}=0)
       ConvArgs<S> ca = conv_args(a);
       ca.dc = a.dcI; ca.raw = a.ci + t * fs; ca.bnstat = bst + (size_t)t * 128;
-      ca.bnb = a.bnbacc + ((size_t)t * 2 + 0) * 64; ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
+      ca.bnb = a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64; ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
       ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
       if (t >= 1) {
         timed(PT_K_CONV_BA, st, [&] {
