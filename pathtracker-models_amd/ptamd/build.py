@@ -1,9 +1,11 @@
 """Build the HIP extensions in-tree for gfx950: ``python -m ptamd.build``.
 
-One ``hipcc -shared -fPIC`` line per library (run in parallel); the resulting
-``libptcell.so`` (InT / hGRU cell, include/pt_cell.h) and ``libptlstm.so``
-(ConvLSTM cell, include/pt_lstm.h) sit next to the ctypes bindings so they
-travel with the repository snapshot to the GPU box.
+One compiler line per library (run in parallel): ``hipcc`` for the gfx950
+kernels — ``libptcell.so`` (InT / hGRU cell, include/pt_cell.h) and
+``libptlstm.so`` (ConvLSTM cell, include/pt_lstm.h) — and ``g++`` for the host
+TFRecord reader ``libpttfr.so`` (include/pt_tfrecord.h, zlib).  They sit next
+to the ctypes bindings so they travel with the repository snapshot to the GPU
+box.
 """
 from __future__ import annotations
 
@@ -22,6 +24,7 @@ LIBS = {
     "libptcell.so": ([os.path.join(CSRC, "pt_cell.hip")],
                      [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
                       os.path.join(INC, "pt_cell.h")]),
+    "libpttfr.so": ([os.path.join(CSRC, "pt_tfrecord.cpp")], [os.path.join(INC, "pt_tfrecord.h")]),
     "libptlstm.so": ([os.path.join(CSRC, "pt_lstm.hip")],
                      [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
                       os.path.join(INC, "pt_lstm.h")]),
@@ -49,8 +52,12 @@ def build(force: bool = False, verbose: bool = True) -> str:
         if not force and up_to_date(lib):
             continue
         out = _out(lib)
-        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I", INC, "-o", out + ".tmp", *srcs]
+        if srcs[0].endswith(".cpp"):
+            cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared",
+                   "-pthread", "-Wall", "-I", INC, "-o", out + ".tmp", *srcs, "-lz"]
+        else:
+            cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                   "-I", INC, "-o", out + ".tmp", *srcs]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((lib, out, subprocess.Popen(cmd)))

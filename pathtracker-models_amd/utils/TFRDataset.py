@@ -1,0 +1,87 @@
+"""TFRDataset — drop-in for the reference ``utils/TFRDataset.py`` without TensorFlow.
+
+Same functions, arguments and batch contents as the reference:
+
+* ``read_tfrecord(example, timesteps=64)`` (:6-28) — one serialized
+  tf.train.Example -> ``(image uint8 [T,32,32,3], label)``;
+* ``tfr_data_loader(data_dir, batch_size=32, drop_remainder=True,
+  shuffle_buffer=1000, timesteps=64)`` (:31-53) — glob -> GZIP TFRecords ->
+  parse -> shuffle(buffer) -> batch(B, drop_remainder).
+
+Decoding runs in the native reader (ptamd/tfrecord.py, libpttfr.so: zlib +
+a minimal protobuf wire decoder, CRC-checked, decoder threads).  Batches are
+numpy arrays that also answer ``.numpy()`` (what the reference's
+``engine.prepare_data`` calls on its TF tensors, utils/engine.py:222-224);
+labels are one-byte strings, so ``np.vectorize(ord)`` works on them as on TF's.
+
+Added for one-process-per-GPU training: the files are sharded by rank
+(file i -> rank i % world; rank / world from torch.distributed when it is
+initialised, else the RANK / WORLD_SIZE environment, else 0 / 1), so every
+rank reads disjoint shards with no scatter.
+"""
+import glob
+import os
+
+import numpy as np
+
+from ptamd import tfrecord
+
+
+class _Batch(np.ndarray):
+    """numpy array with TF's ``.numpy()`` accessor."""
+
+    def numpy(self):
+        return np.asarray(self)
+
+
+def _as_batch(a):
+    return np.asarray(a).view(_Batch)
+
+
+def _rank_world():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+    except ImportError:
+        pass
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def read_tfrecord(example, timesteps=64):
+    """Parse one serialized Example (reference utils/TFRDataset.py:6-28)."""
+    if hasattr(example, "numpy"):
+        example = example.numpy()
+    image, label = tfrecord.parse_example(bytes(example), timesteps)
+    return image, label
+
+
+class _Loader:
+    def __init__(self, files, batch_size, drop_remainder, shuffle_buffer, timesteps, seed):
+        self.files, self.batch_size = files, batch_size
+        self.drop_remainder, self.shuffle_buffer = drop_remainder, shuffle_buffer
+        self.timesteps, self.seed, self.epoch = timesteps, seed, 0
+
+    def __iter__(self):
+        # reshuffle_each_iteration=True: a new shuffle seed per pass (:50)
+        rank, world = _rank_world()
+        rd = tfrecord.Reader(self.files, self.timesteps, rank=rank, world=world,
+                             shuffle_buffer=self.shuffle_buffer, seed=self.seed + self.epoch,
+                             threads=min(8, max(1, len(self.files))),
+                             drop_remainder=self.drop_remainder)
+        self.epoch += 1
+        try:
+            for clips, labels in rd.batches(self.batch_size):
+                yield _as_batch(clips), _as_batch(np.array([bytes([v]) for v in labels], dtype=object))
+        finally:
+            rd.close()
+
+
+def tfr_data_loader(data_dir="", batch_size=32, drop_remainder=True, shuffle_buffer=1000,
+                    timesteps=64, seed=0):
+    """Iterable of ``(images [B,T,32,32,3] uint8, labels [B] 1-byte strings)``
+    (reference utils/TFRDataset.py:31-53)."""
+    if data_dir is None:
+        raise ValueError("Missing path to data directory!")
+    files = sorted(glob.glob(data_dir))
+    return _Loader(files, batch_size, drop_remainder, shuffle_buffer, timesteps, seed)
