@@ -43,8 +43,8 @@ typedef struct pt_cell_desc {
     int32_t batch;      /* B  clips on this device                              */
     int32_t channels;   /* C  = `dimensions` (utils/engine.py:75); must be 32  */
     int32_t frames;     /* T  = x.shape[2]                                      */
-    int32_t height;     /* H  (32)                                              */
-    int32_t width;      /* W  (32)                                              */
+    int32_t height;     /* H  multiple of 32 (32; 64 for hGRU cfg4)             */
+    int32_t width;      /* W  multiple of 32; frames > 32x32 run as 32x32 tiles */
     int32_t ksize;      /* horizontal kernel size, odd, <= 7 (engine default 7) */
     int32_t act;        /* PT_ACT_*                                             */
     int32_t no_inh;     /* InT_no_inh (models/InT.py:168)                       */

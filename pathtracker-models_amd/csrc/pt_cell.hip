@@ -52,6 +52,8 @@ struct CellArgs {
   int hgru;       // hConvGRUCell: the gated inhibition is the attention map (ffhgru_hierarchy.py:147)
   float eps;
   int t;
+  int ntx, nty;   // frames of (32 nty) x (32 ntx) px as nty x ntx tiles of 32x32 ("virtual
+                  // clips": B counts tiles, B = clips * ntx * nty); 1 x 1 at 32x32
   int ablate;     // timing experiments only (env PT_CELL_ABLATE): 1 skip conv MFMAs,
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
                   // atomics, 16 skip the 1x1 weight-gradient LDS reductions,
@@ -82,17 +84,73 @@ struct CellArgs {
 __device__ __forceinline__ size_t fr_off(int t, int B) { return (size_t)t * B * NPIX * C; }
 __device__ __forceinline__ size_t clip_off(int b) { return (size_t)b * NPIX * C; }
 
-// Stage rows [y0, y0+nrows) of x[b, 0:3, t] as float4 per pixel.
-__device__ void stage_x(const float* __restrict__ x, f32x4* xs, int b, int t, int T, int y0,
-                        int nrows, int tid, int nthreads) {
-  const float* x0 = x + ((size_t)(b * 3 + 0) * T + t) * NPIX + y0 * IMG;
-  const float* x1 = x + ((size_t)(b * 3 + 1) * T + t) * NPIX + y0 * IMG;
-  const float* x2 = x + ((size_t)(b * 3 + 2) * T + t) * NPIX + y0 * IMG;
+// Spatial tiling.  A frame larger than 32x32 (H, W multiples of 32) is held as
+// nty x ntx tiles of 32x32, each stored and processed like a clip of its own
+// (tile v = (clip b, row ty, col tx), v = (b nty + ty) ntx + tx).  Point-wise
+// work never looks at neighbours; the k x k convolutions take their 3-px halo
+// from the neighbouring tiles (tile_halo, WBand); BatchNorm's (B, H, W)
+// statistics are the same sums over tiles instead of clips.
+struct TileLoc { int b, ty, tx; };
+__device__ __forceinline__ TileLoc tile_loc(int v, int ntx, int nty) {
+  const int ntl = ntx * nty, b = v / ntl, q = v - b * ntl, ty = q / ntx;
+  return {b, ty, q - ty * ntx};
+}
+
+// Stage rows [y0, y0+nrows) of tile v of x[:, 0:3, t] (x is [clips][3][T][H][W])
+// as float4 per pixel.
+__device__ void stage_x(const float* __restrict__ x, f32x4* xs, int v, int t, int T, int y0,
+                        int nrows, int tid, int nthreads, int ntx, int nty) {
+  const TileLoc L = tile_loc(v, ntx, nty);
+  const int W = ntx * IMG;
+  const size_t plane = (size_t)nty * IMG * W;
+  const size_t o = (size_t)(L.ty * IMG + y0) * W + L.tx * IMG;
+  const float* x0 = x + ((size_t)(L.b * 3 + 0) * T + t) * plane + o;
+  const float* x1 = x + ((size_t)(L.b * 3 + 1) * T + t) * plane + o;
+  const float* x2 = x + ((size_t)(L.b * 3 + 2) * T + t) * plane + o;
   for (int p = tid; p < nrows * IMG; p += nthreads) {
-    f32x4 v;
-    v[0] = x0[p]; v[1] = x1[p]; v[2] = x2[p]; v[3] = 0.f;
-    xs[p] = v;
+    const int q = (p >> 5) * W + (p & 31);
+    f32x4 v4;
+    v4[0] = x0[q]; v4[1] = x1[q]; v4[2] = x2[q]; v4[3] = 0.f;
+    xs[p] = v4;
   }
+}
+
+// Halo of tile v's zero-padded LDS image when the frame has several tiles: the
+// 420 border pixels (3 rows above / below incl. corners, 3 columns left /
+// right) are channel chunks of the neighbouring tiles (ld maps a chunk's
+// element offset to its 16 B, e.g. applying BatchNorm backward); positions
+// outside the frame keep the zeros of tile_zero.
+template <class S, class Ld>
+__device__ __forceinline__ void tile_halo(S* __restrict__ tile, int v, int ntx, int nty, int pass,
+                                          int tid, Ld&& ld) {
+  constexpr int CPB = 16 / (int)sizeof(S);
+  constexpr int NCH = Tr<S>::CP / CPB;
+  constexpr int NHP = TILE * TILE - NPIX;              // 420
+  constexpr int PER = (NHP * NCH + NT - 1) / NT;
+  const TileLoc L = tile_loc(v, ntx, nty);
+  u32x4 val[PER];
+  int dst[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int idx = tid + k * NT;
+    const int hp = idx / NCH, q = idx - hp * NCH;
+    int hy, hx;
+    if (hp < 3 * TILE) { hy = hp / TILE - PADMAX; hx = hp % TILE - PADMAX; }
+    else if (hp < 6 * TILE) { const int j = hp - 3 * TILE; hy = IMG + j / TILE; hx = j % TILE - PADMAX; }
+    else if (hp < 6 * TILE + 3 * IMG) { const int j = hp - 6 * TILE; hy = j / 3; hx = j % 3 - PADMAX; }
+    else { const int j = hp - 6 * TILE - 3 * IMG; hy = j / 3; hx = IMG + j % 3; }
+    const int dy = hy < 0 ? -1 : (hy >= IMG ? 1 : 0), dx = hx < 0 ? -1 : (hx >= IMG ? 1 : 0);
+    const bool ok = idx < NHP * NCH && L.ty + dy >= 0 && L.ty + dy < nty && L.tx + dx >= 0 &&
+                    L.tx + dx < ntx;
+    const int ly = hy - dy * IMG, lx = hx - dx * IMG;
+    const size_t e = clip_off(ok ? v + dy * ntx + dx : v) + (size_t)(ly * IMG + lx) * C +
+                     pass * Tr<S>::CP + q * CPB;
+    val[k] = ld(ok ? e : clip_off(v), pass * Tr<S>::CP + q * CPB);
+    dst[k] = ok ? tile_off<S>(hy + PADMAX, hx + PADMAX, q * CPB) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (dst[k] >= 0) *(u32x4*)(tile + dst[k]) = val[k];
 }
 
 // Stem (models/InT.py:212-213): z = W_pre x + b; xbn = nl(z); CL layout.
@@ -192,6 +250,7 @@ template <class S>
 struct ConvArgs {
   using F = typename Tr<S>::frag;
   int B, K, ablate;
+  int ntx, nty;                 // tiles per frame (halo from neighbours when > 1 x 1)
   const S* src;                 // FILL_COPY: frame base [B][NPIX][C]
   const S* dc;                  // FILL_BNBWD: dy
   const S* raw;                 // FILL_BNBWD: pre-BN conv output of the forward
@@ -240,10 +299,31 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
   if constexpr (EPI != EPI_NONE) tile_zero<S>(tile, tid);
   __syncthreads();
 
+  const bool tiled = a.ntx * a.nty > 1;
+  auto bnbwd16 = [&](const u32x4& dv, const u32x4& rv, int ch0) {
+    constexpr int CPB = 16 / (int)sizeof(S);
+    const S* rr = (const S*)&rv;
+    const S* dd = (const S*)&dv;
+    u32x4 ov;
+    S* oo = (S*)&ov;
+#pragma unroll
+    for (int j = 0; j < CPB; ++j) {
+      const int ch = ch0 + j;
+      oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
+    }
+    return ov;
+  };
   auto fill = [&](int pass) {
     if constexpr (FILL == FILL_COPY) {
+      if (tiled)
+        tile_halo<S>(tile, b, a.ntx, a.nty, pass, tid,
+                     [&](size_t e, int) { return *(const u32x4*)(a.src + e); });
       tile_fill<S>(tile, a.src + cb, pass, tid);
     } else {
+      if (EPI != EPI_NONE && tiled)
+        tile_halo<S>(tile, b, a.ntx, a.nty, pass, tid, [&](size_t e, int ch0) {
+          return bnbwd16(*(const u32x4*)(a.dc + e), *(const u32x4*)(a.raw + e), ch0);
+        });
       constexpr int CPB = 16 / (int)sizeof(S);      // channels per 16-B chunk of S
       constexpr int NCH = Tr<S>::CP / CPB;
       constexpr int PER = NPIX * NCH / NT;           // 16 chunks per thread
@@ -485,7 +565,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
     egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
     cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
   }
-  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
+  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   if (t > 0)
     bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
@@ -524,7 +604,10 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   for (int r = 0; r < 16; ++r) { att[r] = sigm(acc[r] + ba); gEv[r] = att[r] * Ep[r]; }
   store_cl(a.gE + t * fs + ro, c, h, gEv);
   if (a.gates) {
-    float* gp = a.gates + (((size_t)b * T + t) * C + c) * NPIX + y * IMG;
+    const TileLoc tl = tile_loc(b, a.ntx, a.nty);
+    const int W = a.ntx * IMG;
+    float* gp = a.gates + (((size_t)tl.b * T + t) * C + c) * ((size_t)a.nty * IMG * W) +
+                (size_t)(tl.ty * IMG + y) * W + tl.tx * IMG;
 #pragma unroll
     for (int r = 0; r < 16; ++r) gp[cl_x(r, h)] = att[r];
   }
@@ -581,7 +664,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   Pk<S> gi;                    // gated inhibition: I_{t-1} (InT) / att_t (hGRU)
   if constexpr (HG) gi = load_pk(a.at + t * fs + ro, c, h);
   else gi = Iv;
-  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
+  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, B, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
@@ -641,7 +724,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
   slab_prefetch(slab_p, L.slabl, 0, 2, wave, lane);        // a_w, a_u
-  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWA_RPP, tid, PW_NT);
+  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWA_RPP, tid, PW_NT, a.ntx, a.nty);
   gacc_zero(L.gacc, 2, tid);
   __syncthreads();
 
@@ -790,7 +873,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
     civ = load_pk(a.ci + t * fs + ro, c, h);
   }
   slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);        // i_w, i_u, e_w, e_u
-  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT);
+  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   gacc_zero(L.gacc, 4, tid);
   __syncthreads();
 
@@ -926,14 +1009,20 @@ struct WBand {
   static constexpr int NCH = C / CPB;
   static constexpr int XPER = wg_xr<S>() * IMG * NCH / NT;     // 7 (bf16) / 14 (f32)
   static constexpr int DPER = wg_rb<S>() * IMG * NCH / NT;     // 4 / 8
-  u32x4 x[XPER], d[DPER];
-  int xvalid;                                              // bit j: X chunk j inside the image
+  // tiled frames only: the 6 halo columns of the X rows come from the left /
+  // right neighbour tiles (at 32x32 they stay zero from the initial clear)
+  static constexpr int HN = wg_xr<S>() * 2 * PADMAX * NCH;
+  static constexpr int HPER = (HN + NT - 1) / NT;                // 2
+  u32x4 x[XPER], d[DPER], hx[HPER];
+  int xvalid;                                              // bit j: X chunk j inside the frame
+  int hvalid;                                              // bit j: halo chunk j inside the frame
 
   __device__ __forceinline__ void load(const S* __restrict__ Xs, const S* __restrict__ Ds, int B,
-                                       int f, int y0, int tid) {
+                                       int f, int y0, int tid, int ntx, int nty) {
     const int t = f / B, b = f - t * B;
-    const S* xsrc = Xs + ((size_t)t * B + b) * NPIX * C;
+    const S* xfr = Xs + (size_t)t * B * NPIX * C;
     const S* dsrc = Ds + ((size_t)t * B + b) * NPIX * C;
+    const TileLoc L = tile_loc(b, ntx, nty);
     xvalid = 0;
 #pragma unroll
     for (int j = 0; j < XPER; ++j) {
@@ -941,10 +1030,29 @@ struct WBand {
       const int q = idx % NCH, pc = idx / NCH;
       const int col = pc % IMG, row = pc / IMG;
       const int iy = y0 + row - PADMAX;
-      const bool ok = iy >= 0 && iy < IMG;
-      const int cy = ok ? iy : 0;
-      x[j] = *(const u32x4*)(xsrc + (cy * IMG + col) * C + q * CPB);
+      const int dy = iy < 0 ? -1 : (iy >= IMG ? 1 : 0);
+      const bool ok = L.ty + dy >= 0 && L.ty + dy < nty;
+      const int cy = ok ? iy - dy * IMG : 0;
+      x[j] = *(const u32x4*)(xfr + clip_off(ok ? b + dy * ntx : b) + (cy * IMG + col) * C + q * CPB);
       xvalid |= ok << j;
+    }
+    hvalid = 0;
+    if (ntx * nty > 1) {
+#pragma unroll
+      for (int j = 0; j < HPER; ++j) {
+        const int idx = tid + j * NT;
+        const int q = idx % NCH, pc = idx / NCH;
+        const int k = pc % (2 * PADMAX), row = pc / (2 * PADMAX);
+        const int ix = k < PADMAX ? k - PADMAX : IMG + k - PADMAX;
+        const int iy = y0 + row - PADMAX;
+        const int dy = iy < 0 ? -1 : (iy >= IMG ? 1 : 0), dx = ix < 0 ? -1 : 1;
+        const bool ok = idx < HN && L.ty + dy >= 0 && L.ty + dy < nty && L.tx + dx >= 0 &&
+                        L.tx + dx < ntx;
+        const int cy = ok ? iy - dy * IMG : 0, cx = ok ? ix - dx * IMG : 0;
+        hx[j] = *(const u32x4*)(xfr + clip_off(ok ? b + dy * ntx + dx : b) + (cy * IMG + cx) * C +
+                                q * CPB);
+        hvalid |= ok << j;
+      }
     }
 #pragma unroll
     for (int j = 0; j < DPER; ++j) {
@@ -953,7 +1061,7 @@ struct WBand {
       d[j] = *(const u32x4*)(dsrc + (y0 * IMG + pc) * C + q * CPB);
     }
   }
-  __device__ __forceinline__ void store(S* xt, S* dt, int tid) const {
+  __device__ __forceinline__ void store(S* xt, S* dt, int tid, bool tiled) const {
 #pragma unroll
     for (int j = 0; j < XPER; ++j) {
       const int idx = tid + j * NT;
@@ -961,6 +1069,17 @@ struct WBand {
       const int col = pc % IMG, row = pc / IMG;
       const u32x4 z = {0u, 0u, 0u, 0u};
       *(u32x4*)(xt + wx_off(row, col + PADMAX, q * CPB)) = (xvalid >> j) & 1 ? x[j] : z;
+    }
+    if (tiled) {
+#pragma unroll
+      for (int j = 0; j < HPER; ++j) {
+        const int idx = tid + j * NT;
+        const int q = idx % NCH, pc = idx / NCH;
+        const int k = pc % (2 * PADMAX), row = pc / (2 * PADMAX);
+        const int col = k < PADMAX ? k : IMG + k;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        if (idx < HN) *(u32x4*)(xt + wx_off(row, col, q * CPB)) = (hvalid >> j) & 1 ? hx[j] : z;
+      }
     }
 #pragma unroll
     for (int j = 0; j < DPER; ++j) {
@@ -1024,8 +1143,10 @@ __device__ __forceinline__ void wgrad_band(f32x16 (&acc)[WG_NACC], const S* xt, 
 template <class S, int K>
 __device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __restrict__ Xs,
                                           const S* __restrict__ Ds, int B, int T, int g, int nwg,
-                                          S* buf, int tid, int lane, int wave, int ablate) {
+                                          S* buf, int tid, int lane, int wave, int ablate, int ntx,
+                                          int nty) {
   constexpr int KK = K * K;
+  const bool tiled = ntx * nty > 1;
   // wave-uniform element offset of each tap; taps beyond K*K (the 13th slot of
   // waves 1-3 at K=7) read tap 0 and their accumulator is never stored, so
   // every MFMA is unconditional (no accumulator copies around branches)
@@ -1046,8 +1167,8 @@ __device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __res
   __syncthreads();
   WBand<S> band;
   if (nunits > 0) {
-    band.load(Xs, Ds, B, g, 0, tid);
-    band.store(buf, buf + wg_xr<S>() * TILE * C, tid);
+    band.load(Xs, Ds, B, g, 0, tid, ntx, nty);
+    band.store(buf, buf + wg_xr<S>() * TILE * C, tid, tiled);
   }
   __syncthreads();
   for (int u = 0; u < nunits; ++u) {
@@ -1055,11 +1176,11 @@ __device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __res
     S* dt = xt + wg_xr<S>() * TILE * C;
     const bool more = u + 1 < nunits;
     if (more && !(ablate & 128))
-      band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * wg_rb<S>(), tid);
+      band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * wg_rb<S>(), tid, ntx, nty);
     if (!(ablate & 64)) wgrad_band<S, K>(acc, xt, dt, toff, lane);
     if (more) {
       S* xn = buf + ((u + 1) & 1) * BE;
-      if (!(ablate & 128)) band.store(xn, xn + wg_xr<S>() * TILE * C, tid);
+      if (!(ablate & 128)) band.store(xn, xn + wg_xr<S>() * TILE * C, tid, tiled);
       __syncthreads();
     }
   }
@@ -1087,10 +1208,10 @@ __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, in
 #pragma unroll
   for (int m = 0; m < WG_NACC; ++m) acc[m] = zero16();
   switch (a.K) {
-    case 7: wgrad_run<S, 7>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
-    case 5: wgrad_run<S, 5>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
-    case 3: wgrad_run<S, 3>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
-    default: wgrad_run<S, 1>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate); break;
+    case 7: wgrad_run<S, 7>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
+    case 5: wgrad_run<S, 5>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
+    case 3: wgrad_run<S, 3>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
+    default: wgrad_run<S, 1>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
   }
   // acc[m]: rows ci = cl_x(r,h), cols n = lane&31
   float* dst = wslab + ((size_t)conv * nwg + g) * MAXTAP * 1024;
@@ -1234,21 +1355,29 @@ __global__ void k_reduce(ReduceArgs r) {
   }
 }
 
-// channels-last [B][32][32][C] (S)  <->  NCHW fp32
+// channels-last tiles [B tiles][32][32][C] (S)  <->  NCHW fp32 frames
+__device__ __forceinline__ size_t nchw_off(int v, int pix, int c, int T, int t, int ntx, int nty) {
+  const TileLoc L = tile_loc(v, ntx, nty);
+  const int W = ntx * IMG;
+  return (((size_t)L.b * T + t) * C + c) * ((size_t)nty * IMG * W) +
+         (size_t)(L.ty * IMG + (pix >> 5)) * W + L.tx * IMG + (pix & 31);
+}
 template <class S>
-__global__ void k_to_nchw(const S* __restrict__ src, float* __restrict__ dst, int B, int T, int t) {
-  // dst [B][T][C][NPIX] (T=1,t=0 for a single frame)
+__global__ void k_to_nchw(const S* __restrict__ src, float* __restrict__ dst, int B, int T, int t,
+                          int ntx, int nty) {
+  // dst [clips][T][C][H][W] (T=1,t=0 for a single frame); B = tiles
   const int n = B * NPIX * C;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const int c = e % C, pix = (e / C) % NPIX, b = e / (C * NPIX);
-    dst[(((size_t)b * T + t) * C + c) * NPIX + pix] = ldf(src + e);
+    const int c = e % C, pix = (e / C) % NPIX, v = e / (C * NPIX);
+    dst[nchw_off(v, pix, c, T, t, ntx, nty)] = ldf(src + e);
   }
 }
-__global__ void k_from_nchw(const float* __restrict__ src, float* __restrict__ dst, int B) {
+__global__ void k_from_nchw(const float* __restrict__ src, float* __restrict__ dst, int B, int ntx,
+                            int nty) {
   const int n = B * NPIX * C;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const int c = e % C, pix = (e / C) % NPIX, b = e / (C * NPIX);
-    dst[e] = src[((size_t)b * C + c) * NPIX + pix];
+    const int c = e % C, pix = (e / C) % NPIX, v = e / (C * NPIX);
+    dst[e] = src[nchw_off(v, pix, c, 1, 0, ntx, nty)];
   }
 }
 
@@ -1308,6 +1437,7 @@ inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Plan {
   int B, T, K, dt;
+  int ntx, nty;       // tiles per frame; B counts tiles (clips * ntx * nty)
   size_t es;          // element size of S
   size_t frame;       // elements per frame tensor (B*NPIX*C)
   // saved offsets
@@ -1320,8 +1450,10 @@ struct Plan {
 int check(const pt_cell_desc* d) {
   if (!d) return fail(PT_ERR_ARG, "null descriptor%s%ld");
   if (d->channels != 32) return fail(PT_ERR_UNSUPPORTED, "channels must be 32 (got %s%ld)", "", d->channels);
-  if (d->height != 32 || d->width != 32)
-    return fail(PT_ERR_UNSUPPORTED, "only 32x32 frames are supported%s (H=%ld)", "", d->height);
+  if (d->height < 32 || d->height % 32 || d->height > 1024)
+    return fail(PT_ERR_UNSUPPORTED, "height must be a multiple of 32 in [32, 1024]%s (got %ld)", "", d->height);
+  if (d->width < 32 || d->width % 32 || d->width > 1024)
+    return fail(PT_ERR_UNSUPPORTED, "width must be a multiple of 32 in [32, 1024]%s (got %ld)", "", d->width);
   if (d->ksize < 1 || d->ksize > 7 || (d->ksize & 1) == 0)
     return fail(PT_ERR_UNSUPPORTED, "ksize must be odd and <= 7%s (got %ld)", "", d->ksize);
   if (d->batch < 1 || d->frames < 1) return fail(PT_ERR_ARG, "batch and frames must be >= 1%s%ld");
@@ -1334,7 +1466,8 @@ int check(const pt_cell_desc* d) {
 
 Plan plan(const pt_cell_desc* d) {
   Plan p{};
-  p.B = d->batch; p.T = d->frames; p.K = d->ksize; p.dt = d->dtype;
+  p.ntx = d->width / IMG; p.nty = d->height / IMG;
+  p.B = d->batch * p.ntx * p.nty; p.T = d->frames; p.K = d->ksize; p.dt = d->dtype;
   p.es = d->dtype == PT_DTYPE_BF16 ? 2 : 4;
   p.frame = (size_t)p.B * NPIX * C;
   const size_t fbytes = al(p.frame * p.T * p.es);
@@ -1369,6 +1502,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
   using F = typename Tr<S>::frag;
   memset(&a, 0, sizeof(a));
   a.B = p.B; a.T = p.T; a.K = p.K; a.act = d->act; a.no_inh = d->no_inh; a.eps = d->eps;
+  a.ntx = p.ntx; a.nty = p.nty;
   a.hgru = d->cell == PT_CELL_HGRU;
   a.x = x;
   {
@@ -1455,6 +1589,7 @@ ConvArgs<S> conv_args(const CellArgs<S>& a) {
   ConvArgs<S> c;
   memset(&c, 0, sizeof(c));
   c.B = a.B; c.K = a.K; c.ablate = a.ablate;
+  c.ntx = a.ntx; c.nty = a.nty;
   return c;
 }
 
@@ -1499,7 +1634,7 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   }
   if (e_last)
     hipLaunchKernelGGL(k_to_nchw<S>, dim3(256), dim3(256), 0, st,
-                       (const S*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0);
+                       (const S*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0, p.ntx, p.nty);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1515,7 +1650,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   HIPCHK(hipMemsetAsync((char*)ws + p.o_slab, 0, (size_t)p.B * PW_PARTS * SLAB * 4, st));
   HIPCHK(hipMemsetAsync((char*)ws + p.o_bnbacc, 0, (size_t)p.T * 2 * NBNC * 64 * 8, st));
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
-                     (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B);
+                     (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
   const size_t lpa = (pw_lds_bytes<PWA_RPP, true>()), lpb = (pw_lds_bytes<PWB_RPP, true>());
   const size_t lcv = conv_lds_bytes<S>();
@@ -1622,10 +1757,10 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, p
   for (int t = 0; t < p.T; ++t) {
     if (d->dtype == PT_DTYPE_BF16)
       hipLaunchKernelGGL(k_to_nchw<bf16_t>, dim3(256), dim3(256), 0, (hipStream_t)stream,
-                         (const bf16_t*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B, p.T, t);
+                         (const bf16_t*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B, p.T, t, p.ntx, p.nty);
     else
       hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, (hipStream_t)stream,
-                         (const float*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B, p.T, t);
+                         (const float*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B, p.T, t, p.ntx, p.nty);
   }
   HIPCHK(hipGetLastError());
   return 0;

@@ -106,7 +106,7 @@ def run_recurrent(model, x, y, want_gates):
 
 
 def make_int(ref_int, tag, *, batch, t_len, dims, act="softplus", no_inh=False,
-             lesion=(), want_gates=True, seed=0):
+             lesion=(), want_gates=True, seed=0, hw=(32, 32)):
     synth = _synth()
     torch.manual_seed(1000 + seed)
     kw = dict(dimensions=dims, timesteps=t_len, kernel_size=7, jacobian_penalty=False,
@@ -121,7 +121,7 @@ def make_int(ref_int, tag, *, batch, t_len, dims, act="softplus", no_inh=False,
         with torch.no_grad():
             model.unit1.alpha.fill_(1.0)
             model.unit1.mu.fill_(0.0)
-    clips, labels = synth.make_batch(seed, batch, t_len)
+    clips, labels = synth.make_batch(seed, batch, t_len, h=hw[0], w=hw[1])
     x, y = prepare(clips, labels)
     out = run_recurrent(model, x, y, want_gates)
     out.update(clip_u8=clips, label_u8=np.array([ord(b) for b in labels], np.uint8),
@@ -133,13 +133,13 @@ def make_int(ref_int, tag, *, batch, t_len, dims, act="softplus", no_inh=False,
           "loss", float(out["loss"]))
 
 
-def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0, want_gates=True):
+def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0, want_gates=True, hw=(32, 32)):
     synth = _synth()
     torch.manual_seed(2000 + seed)
     model = ref_hgru.FFhGRU(dimensions=dims, timesteps=t_len, kernel_size=7,
                             jacobian_penalty=False, grad_method="bptt")
     perturb_recurrent(model, seed)
-    clips, labels = synth.make_batch(seed + 7, batch, t_len)
+    clips, labels = synth.make_batch(seed + 7, batch, t_len, h=hw[0], w=hw[1])
     x, y = prepare(clips, labels)
     out = run_recurrent(model, x, y, want_gates)
     out.update(clip_u8=clips, label_u8=np.array([ord(b) for b in labels], np.uint8),
@@ -249,6 +249,12 @@ def main():
             "hgru_c32": lambda: make_hgru(ref_hgru, "hgru_c32", batch=2, t_len=6, dims=32, seed=6),
             "hgru_b4t16": lambda: make_hgru(ref_hgru, "hgru_b4t16", batch=4, t_len=16, dims=32,
                                             seed=8, want_gates=False),
+            # cfg4's 64x64 frames (ffhgru_hierarchy long-range), and a non-square
+            # frame whose middle tiles have neighbours on every side
+            "hgru_64": lambda: make_hgru(ref_hgru, "hgru_64", batch=2, t_len=4, dims=32,
+                                         seed=11, hw=(64, 64)),
+            "int_64x96": lambda: make_int(ref_int, "int_64x96", batch=2, t_len=3, dims=32,
+                                          seed=12, hw=(64, 96)),
             "init_convlstm_seed123": lambda: make_init_convlstm(ref_clstm, "init_convlstm_seed123"),
             "convlstm_k7": lambda: make_convlstm(ref_clstm, "convlstm_k7", batch=2, timesteps=4,
                                                  filt=7, seed=7),

@@ -14,8 +14,8 @@ from goldens import cfg, load, params, prepared_input
 
 pytestmark = pytest.mark.gpu
 
-INT_TAGS = ["int_c32", "int_tanh", "int_lesion", "int_noinh", "int_cfg1"]
-HGRU_TAGS = ["hgru_c32", "hgru_b4t16"]
+INT_TAGS = ["int_c32", "int_tanh", "int_lesion", "int_noinh", "int_cfg1", "int_64x96"]
+HGRU_TAGS = ["hgru_c32", "hgru_b4t16", "hgru_64"]
 
 
 def _dev():
@@ -101,7 +101,7 @@ def test_bptt_grads_and_adam_f32(tag):
         _assert_close(f"adam {k}", p.detach().cpu(), g["adam." + k], 1e-6, 1e-3)
 
 
-@pytest.mark.parametrize("tag", ["int_c32", "int_cfg1", "hgru_c32"])
+@pytest.mark.parametrize("tag", ["int_c32", "int_cfg1", "hgru_c32", "hgru_64"])
 def test_forward_bf16_tolerance(tag):
     """bf16 operands / saved states, f32 accumulation: logits within 5e-2 and
     per-frame states within 5e-2 of the reference after up to 32 recurrent steps."""

@@ -60,6 +60,15 @@ def test_size_queries_and_validation():
     assert b"channels" in lib.pt_last_error()
     bad.channels, bad.ksize = 32, 4
     assert lib.pt_cell_saved_bytes(ctypes.byref(bad)) == 0
+    # frames larger than 32x32 run as 32x32 tiles: sizes scale with the tile count
+    # (cfg4: hGRU 64x64x128f, 128 clips per GPU); sides must be multiples of 32
+    big = _lib.Desc(batch=128, channels=32, frames=128, height=64, width=64, ksize=7, act=0,
+                    no_inh=0, cell=1, dtype=_lib.PT_DTYPE_BF16, eps=1e-3)
+    assert lib.pt_cell_saved_bytes(ctypes.byref(big)) >= 7 * 128 * (128 * 4096 * 32 * 2)
+    for h, w in ((48, 64), (64, 40), (16, 32)):
+        big.height, big.width = h, w
+        assert lib.pt_cell_saved_bytes(ctypes.byref(big)) == 0
+        assert b"multiple of 32" in lib.pt_last_error()
 
 
 @pytest.mark.parametrize("tag", ["int_c32", "int_noinh", "int_lesion"])
