@@ -392,23 +392,26 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
 }
 
 // =========================================================================
-// Point-wise kernels: 8 waves per workgroup, each wave owns PW_RPP image rows
-// (1 in the forward, 2 in the backward), several workgroups per CU: the long
-// dependent element-wise / 1x1-gate chains are hidden by occupancy.
+// Point-wise kernels: 4 waves per workgroup, each wave owns PW_RPP image rows
+// (1 in k_pw_fa / k_pw_fb / k_pw_bb, 4 in k_pw_ba), several workgroups per CU:
+// the long dependent element-wise / 1x1-gate chains and the workgroup barriers
+// of one workgroup are hidden behind the others (the backward kernels need
+// 256 VGPRs, i.e. 2 waves per SIMD: with 8-wave workgroups one workgroup
+// filled a CU; 4-wave workgroups measured k_pw_bb 68.4 -> 66.0 us, k_pw_ba
+// 57.7 -> 55.2 us).
 // =========================================================================
-constexpr int PW_NT = 512;
+constexpr int PW_NT = 256;
 constexpr int PW_NW = PW_NT / 64;
 constexpr int PWF_RPP = 1;                         // forward rows per wave
-// k_pw_ba takes a whole clip per workgroup (4 rows per wave, in a loop): its
-// fixed per-workgroup cost (slab prefetch / flush, x staging, LDS clears,
-// reductions) is paid once per clip (measured 59.3 -> 56.8 us per launch).
+// k_pw_ba loops over 4 rows per wave: its fixed per-workgroup cost (slab
+// prefetch / flush, x staging, LDS clears, reductions) is paid once per 16 rows.
 // k_pw_bb stays at one row per wave: looping its body spills (~46 VGPRs) and
 // doubled its row cost.
 constexpr int PWA_RPP = 4;                         // k_pw_ba rows per wave
 constexpr int PWB_RPP = 1;                         // k_pw_bb rows per wave (register bound)
-constexpr int PWF_WGPC = IMG / (PW_NW * PWF_RPP);  // workgroups per clip (4)
-constexpr int PWA_WGPC = IMG / (PW_NW * PWA_RPP);  // (1)
-constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (4)
+constexpr int PWF_WGPC = IMG / (PW_NW * PWF_RPP);  // workgroups per clip (8)
+constexpr int PWA_WGPC = IMG / (PW_NW * PWA_RPP);  // (2)
+constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (8)
 constexpr int PW_PARTS = PWB_WGPC > PWA_WGPC ? PWB_WGPC : PWA_WGPC;   // slab partitions per clip
 
 constexpr int PW_NGACC = 4;   // 1x1 weight-gradient tiles accumulated in LDS per workgroup
@@ -418,7 +421,7 @@ constexpr int pw_lds_bytes() {   // forward point-wise kernels use xs, scr, stat
              ? PW_NW * RPP * IMG * 16 + PW_NW * SCR_FLOATS * 4 + 128 * 4
              : PW_NW * RPP * IMG * 16 /*xs*/ + PW_NW * SCR_FLOATS * 4 /*scr*/ + 128 * 4 /*stat*/ +
                    PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ +
-                   PW_NGACC * 1024 * 4 /*gacc*/ + PW_NW * 1024 * 4 /*flush*/ + SLAB * 4 /*slab copy*/;
+                   PW_NGACC * 1024 * 4 /*gacc*/ + SLAB * 4 /*slab copy*/;
 }
 struct PLds {
   f32x4* xs;
@@ -427,7 +430,7 @@ struct PLds {
   float* small;   // [PW_NW][NSMALL][32]
   float* red;     // [512]
   float* gacc;    // [PW_NGACC][1024]  (rows n, cols ci)
-  float* flush;   // [PW_NW][1024]     per-wave weight-gradient tiles of one gate
+  float* flush;   // [PW_NW][SCR_FLOATS] per-wave weight-gradient tiles of one gate (aliases scr)
   float* slabl;   // [SLAB]            this workgroup's slab partition, prefetched
 };
 template <int RPP>
@@ -439,8 +442,8 @@ __device__ __forceinline__ PLds pcarve(char* smem) {
   l.small = l.stat + 128;
   l.red = l.small + PW_NW * NSMALL * 32;
   l.gacc = l.red + 512;
-  l.flush = l.gacc + PW_NGACC * 1024;
-  l.slabl = l.flush + PW_NW * 1024;
+  l.flush = l.scr;       // gacc_row runs between a wave's transposes, fenced by barriers
+  l.slabl = l.gacc + PW_NGACC * 1024;
   return l;
 }
 
@@ -454,12 +457,12 @@ __device__ __forceinline__ void gacc_row(float* gacc_g, float* flush, const f32x
   const f32x16 t = wgrad_cl<S>(d, x, zero16());
   const int ci = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) flush[wave * 1024 + cl_x(r, h) * 32 + ci] = t[r];
+  for (int r = 0; r < 16; ++r) flush[wave * SCR_FLOATS + cl_x(r, h) * 32 + ci] = t[r];
   __syncthreads();
   for (int e = tid; e < 1024; e += PW_NT) {
     float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < PW_NW; ++w) s += flush[w * 1024 + e];
+    for (int w = 0; w < PW_NW; ++w) s += flush[w * SCR_FLOATS + e];
     gacc_g[e] += s;
   }
   __syncthreads();

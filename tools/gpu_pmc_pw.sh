@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-python __graft_entry__.py build > gpurun_out/p_build.log 2>&1 || { echo BUILD_FAIL; exit 1; }
+# libraries are prebuilt in-tree
 i=0
 for ctrs in "SQ_WAVES SQ_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
             "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU" \
