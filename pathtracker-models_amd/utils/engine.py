@@ -15,6 +15,8 @@ runs unchanged.  Differences, all deliberate:
   hGRU-SEG baselines) are out of scope here and raise ``NotImplementedError``
   with the reference's own message.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -120,3 +122,62 @@ def prepare_data(imgs, target, args, device, disentangle_channels, use_augmentat
         t = np.asarray(target)
         codes = torch.from_numpy(np.vectorize(ord)(t) if t.dtype.kind in 'OSU' else t.astype(np.int64))
     return x, codes.to(device, dtype=torch.float)
+
+
+def load_ckpt(model, model_path):
+    """Load weights (utils/engine.py:258-269).  The reference reads
+    ``checkpoint['state_dict']``, a key its own EarlyStopping files lack
+    (SURVEY.md §5); both forms are accepted here, and a DataParallel
+    ``module.`` prefix is stripped.  Loaded with ``weights_only=True``."""
+    checkpoint = torch.load(model_path, map_location="cpu", weights_only=True)
+    sd = checkpoint['state_dict'] if 'state_dict' in checkpoint else checkpoint
+    sd = {(k[len('module.'):] if k.startswith('module.') else k): v for k, v in sd.items()}
+    model.load_state_dict(sd)
+    return model
+
+
+LOCAL = "/gpfs/data/tserre/data/tracking/tfrecords"
+_CIFS = "/cifs/data/tserre_lrs/projects/prj_tracking"
+
+
+def _rb(length):
+    return f"downsampled_constrained_red_blue_datasets_{length}_32_32_separate_channels"
+
+
+def dataset_selector(dist, speed, length, optical_flow=False, data_root=None):
+    """(tfrecord root, timesteps, len_train_loader, len_val_loader) for a
+    PathTracker variant (utils/engine.py:345-404), same table and quirks: the
+    32-frame sets found on local storage report 64 timesteps (:363,370,377).
+    ``data_root`` (added) overrides the cluster paths; timesteps = length."""
+    if data_root is not None:
+        return os.path.join(data_root, ''), length, 20000, 20000
+    stem = "tfrecords_optic_flow" if optical_flow else "tfrecords"
+
+    def local_or(local_rel, remote, t_remote, t_local=64):
+        lp = os.path.join(LOCAL, local_rel)
+        if os.path.exists(lp):
+            print("Loading data from local storage.")
+            return lp, t_local, 20000, 20000
+        return remote, t_remote, 20000, 20000
+
+    key = (dist, speed, length)
+    if key == (14, 1, 64):
+        # the reference falls back to the 5_dist remote set here (:352-357)
+        return local_or(f"{_rb(64)}/14_dist/tfrecords/", f"{_CIFS}/{_rb(64)}/5_dist/tfrecords/", 64)
+    if key in ((14, 1, 32), (5, 1, 32), (0, 1, 32)):
+        return local_or(f"{_rb(32)}/{dist}_dist/tfrecords/", f"{_CIFS}/{_rb(32)}/{dist}_dist/tfrecords/", 32)
+    if key == (14, 1, 128):
+        return f"{_CIFS}/{_rb(128)}/14_dist/tfrecords/", 128, 20000, 20000
+    if key == (25, 1, 64):
+        return f"{_CIFS}/{_rb(64)}/25_dist/tfrecords/", 64, 20000, 20000
+    if key in ((14, 2, 64), (14, 4, 64)):
+        return f"{_CIFS}/{_rb(64)}_skip_param_{speed}/14_dist/tfrecords/", 64, 20000, 20000
+    if key == (0, 1, 64):
+        return local_or(f"{_rb(64)}/0_dist/{stem}/", f"{_CIFS}/{_rb(64)}/0_dist/tfrecords/", 64)
+    if key == (5, 1, 64):
+        return local_or(f"{_rb(64)}/5_dist/{stem}/", f"{_CIFS}/{_rb(64)}/5_dist/tfrec/{stem}/", 64)
+    return None          # the reference falls off its if/elif chain (returns None)
+
+
+def get_datasets():
+    return ALL_DATASETS

@@ -32,3 +32,24 @@ def acc_scores(target, prediction, threshold=0.5):
     pred = (prediction.reshape(-1) > threshold).byte()
     balacc, precision, recall, f1s = metric_scores(target, pred)
     return balacc * 100, precision, recall, f1s
+
+
+class AverageMeter(object):
+    """Current value, running average and history (misc_functions.py:117-135)."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.history = []
+        self.val = 0
+        self.avg = 0
+        self.sum = 0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.history.append(val)
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count
