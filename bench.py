@@ -72,8 +72,11 @@ def algorithmic_flops(kind, batch, frames):
         "k_pw_ba": (frames - 1) * 4 * gf,           # a_* dgrad + wgrad
         "k_pw_bb": frames * 8 * gf,                 # i_*, e_* dgrad + wgrad
         "k_wgrad": frames * 2 * cf,                 # dW_inh + dW_exc
-    }.get(kind, 0)
-    return per_clip * batch
+    }
+    # fused backward steps = their two halves
+    per_clip["k_conv_pw_bb"] = per_clip["k_conv_bb"] + per_clip["k_pw_bb"]
+    per_clip["k_conv_pw_ba"] = per_clip["k_conv_ba"] + per_clip["k_pw_ba"]
+    return per_clip.get(kind, 0) * batch
 
 
 def algorithmic_bytes(kind, batch, frames, elt):
@@ -91,8 +94,12 @@ def algorithmic_bytes(kind, batch, frames, elt):
         "k_pw_bb": frames * (XF + 9 * F),
         "k_conv_bb": frames * 6 * F,
         "k_wgrad": frames * 4 * F,
-    }.get(kind, 0)
-    return per_clip * batch
+    }
+    # fused backward steps: both halves minus the hand-off tensor (dI_t / dgE_t)
+    # that the point-wise half re-reads from L2 in the same workgroup
+    per_clip["k_conv_pw_bb"] = per_clip["k_conv_bb"] + per_clip["k_pw_bb"] - frames * F
+    per_clip["k_conv_pw_ba"] = per_clip["k_conv_ba"] + per_clip["k_pw_ba"] - (frames - 1) * F
+    return per_clip.get(kind, 0) * batch
 
 
 def pmc_traffic(kernel, batch, frames, dtype):

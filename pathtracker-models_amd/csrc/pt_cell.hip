@@ -24,6 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 namespace ptc {
@@ -55,6 +56,7 @@ struct CellArgs {
   int ntx, nty;   // frames of (32 nty) x (32 ntx) px as nty x ntx tiles of 32x32 ("virtual
                   // clips": B counts tiles, B = clips * ntx * nty); 1 x 1 at 32x32
   int ablate;     // timing experiments only (env PT_CELL_ABLATE): 1 skip conv MFMAs,
+                  // 256 skip the conv epilogue, 512 return at entry (launch floor),
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
                   // atomics, 16 skip the 1x1 weight-gradient LDS reductions,
                   // 32 skip slab flush
@@ -270,16 +272,15 @@ template <class S>
 constexpr int conv_lds_bytes() { return tile_bytes<S>() + CONV_MISC * 4 + 2 * WSLICE_BYTES; }
 
 template <class S, int FILL, int EPI>
-__global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b) {
   S* tile = (S*)smem;
   float* red = (float*)(smem + tile_bytes<S>());
   float* tbl = red + 128;       // FILL_BNBWD: per-channel A, Bc, Cc
   char* wbuf = (char*)(red + CONV_MISC);   // 2 weight slices
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x;
   const size_t cb = clip_off(b);
+  if (a.ablate & 512) return;
 
   if constexpr (FILL == FILL_BNBWD) {
     if (tid < 32) {
@@ -372,11 +373,15 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
 #pragma unroll
     for (int i = 0; i < RPW; ++i) acc[i] = zero16();
     conv_run<S>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate);
+    if (a.ablate & 256) return;
     const int px = lane & 31;
     if constexpr (EPI == EPI_FWD) {
 #pragma unroll
-      for (int i = 0; i < RPW; ++i)
-        store_pl(a.out_raw + cb + ((size_t)(wave * RPW + i) * IMG + px) * C, h, acc[i]);
+      for (int i = 0; i < RPW; ++i) {
+        if (a.ablate & 2048) continue;
+        if (a.ablate & 1024) store_pl_nt(a.out_raw + cb + ((size_t)(wave * RPW + i) * IMG + px) * C, h, acc[i]);
+        else store_pl(a.out_raw + cb + ((size_t)(wave * RPW + i) * IMG + px) * C, h, acc[i]);
+      }
       if (!(a.ablate & 8)) bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
     } else {
 #pragma unroll
@@ -385,10 +390,16 @@ __global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
         f32x16 v = acc[i];
         add_pl(a.add0 + po, h, v);
         if (a.add1) add_pl(a.add1 + po, h, v);
-        store_pl(a.out + po, h, v);
+        if (a.ablate & 1024) store_pl_nt(a.out + po, h, v);
+        else store_pl(a.out + po, h, v);
       }
     }
   }
+}
+template <class S, int FILL, int EPI>
+__global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_body<S, FILL, EPI>(a, smem, blockIdx.x);
 }
 
 // =========================================================================
@@ -550,6 +561,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   static_assert(PWF_RPP == 1, "forward point-wise kernels: one row per wave");
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.ablate & 512) return;
   const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -642,6 +654,7 @@ template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   using F = typename Tr<S>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.ablate & 512) return;
   const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -710,16 +723,16 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
 //     (:175, :173) -> d_eg, dc_e (-> BN1 bwd sums), kappa/gamma grads,
 //     dI_t (local), dE_{t-1} partial = (1-eg) dE_t.
 // -------------------------------------------------------------------------
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
+// Body shared by k_pw_ba (RPP = PWA_RPP rows per wave, PWA_WGPC workgroups per
+// clip) and the fused k_conv_pw_ba (RPP = 8: the conv workgroup's whole clip).
+template <class S, int ACT, int HG, int RPP>
+__device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int b, int part) {
   using F = typename Tr<S>::frag;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const PLds L = pcarve<PWA_RPP>(smem);
+  const PLds L = pcarve<RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x / PWA_WGPC, part = blockIdx.x % PWA_WGPC;
   const int t = a.t, T = a.T, B = a.B;
-  const int y0 = part * PW_NW * PWA_RPP;
+  const int y0 = part * PW_NW * RPP;
   float* wscr = L.scr + wave * SCR_FLOATS;
   const size_t fs = fr_off(1, B), cb = clip_off(b);
   const int tt = t + 1;
@@ -727,7 +740,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
   slab_prefetch(slab_p, L.slabl, 0, 2, wave, lane);        // a_w, a_u
-  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * PWA_RPP, tid, PW_NT, a.ntx, a.nty);
+  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   gacc_zero(L.gacc, 2, tid);
   __syncthreads();
 
@@ -743,8 +756,8 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   const S* dgsrc = a.conv_done ? a.dgE : a.dgEp;
 
 #pragma unroll 1
-  for (int i = 0; i < PWA_RPP && !(a.ablate & 4); ++i) {
-    const int yl = wave * PWA_RPP + i, y = y0 + yl;
+  for (int i = 0; i < RPP && !(a.ablate & 4); ++i) {
+    const int yl = wave * RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 GE;
     if (tail) {
@@ -831,6 +844,12 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
   if (tail && (head || HG) && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
 }
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.ablate & 512) return;
+  pw_ba_body<S, ACT, HG, PWA_RPP>(a, smem, blockIdx.x / PWA_WGPC, blockIdx.x % PWA_WGPC);
+}
 
 // -------------------------------------------------------------------------
 // Backward point-wise B (frame t): with dI_t (= conv^T(dce, w_exc) + local
@@ -839,44 +858,53 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 //   dx_t partial, dI_{t-1}; exc gate backward (:171) -> e_w/e_u grads,
 //   dI_{t-1}, dgE partial.
 // -------------------------------------------------------------------------
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
-  static_assert(PWB_RPP == 1, "k_pw_bb: one row per wave");
+template <class S>
+struct BbRow { Pk<S> ginh, Iprev, dep, gEv, dIt, civ; };
+
+// Body shared by k_pw_bb (RPP = 1 row per wave, PWB_WGPC workgroups per clip)
+// and the fused k_conv_pw_bb (RPP = 8: the conv workgroup's whole clip).
+template <class S, int ACT, int HG, int RPP>
+__device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int b, int part) {
   using F = typename Tr<S>::frag;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const PLds L = pcarve<PWB_RPP>(smem);
+  const PLds L = pcarve<RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x / PWB_WGPC, part = blockIdx.x % PWB_WGPC;
   const int t = a.t, T = a.T, B = a.B;
-  const int y0 = part * PW_NW;
-  const int yl = wave, y = y0 + yl;
+  const int y0 = part * PW_NW * RPP;
   float* wscr = L.scr + wave * SCR_FLOATS;
-  const size_t fs = fr_off(1, B), ro = clip_off(b) + (size_t)y * IMG * C;
+  const size_t fs = fr_off(1, B);
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
-  // row tiles first (their latency overlaps the staging): g_inh = I_{t-1}
-  // (InT) / E_{t-1} (no_inh) and gE_t feed the exc gate (:171), dI_t and c_i
-  // the inhibition backward.  Kept packed; e_w^T d_e_pre is folded into
-  // dI_{t-1} at the end from its A fragments (pe) rather than kept as a tile.
-  // hGRU: g_inh = att_t (ffhgru_hierarchy.py:147) and I_{t-1} is a separate tile
-  Pk<S> ginh, Iprev;
-  if constexpr (HG) {
-    ginh = load_pk(a.at + t * fs + ro, c, h);
-    Iprev = t == 0 ? zero_pk<S>() : load_pk(a.I + (t - 1) * fs + ro, c, h);
-  } else {
-    ginh = t == 0 ? zero_pk<S>()
-                  : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
-  }
-  const Pk<S> dep = load_pk(a.dEp + ro, c, h);
-  const Pk<S> gEv = load_pk(a.gE + t * fs + ro, c, h);
-  Pk<S> dIt = zero_pk<S>(), civ = zero_pk<S>();
-  if (!a.no_inh) {
-    dIt = load_pk(a.dIt + ro, c, h);
-    civ = load_pk(a.ci + t * fs + ro, c, h);
-  }
+  // row tiles: g_inh = I_{t-1} (InT) / E_{t-1} (no_inh) and gE_t feed the exc
+  // gate (:171), dI_t and c_i the inhibition backward.  Kept packed; e_w^T
+  // d_e_pre is folded into dI_{t-1} at the end from its A fragments (pe)
+  // rather than kept as a tile.  hGRU: g_inh = att_t (ffhgru_hierarchy.py:147)
+  // and I_{t-1} is a separate tile.
+  auto load_row = [&](size_t ro) {
+    BbRow<S> w;
+    w.Iprev = zero_pk<S>();
+    if constexpr (HG) {
+      w.ginh = load_pk(a.at + t * fs + ro, c, h);
+      if (t > 0) w.Iprev = load_pk(a.I + (t - 1) * fs + ro, c, h);
+    } else {
+      w.ginh = t == 0 ? zero_pk<S>()
+                      : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
+    }
+    w.dep = load_pk(a.dEp + ro, c, h);
+    w.gEv = load_pk(a.gE + t * fs + ro, c, h);
+    w.dIt = zero_pk<S>();
+    w.civ = zero_pk<S>();
+    if (!a.no_inh) {
+      w.dIt = load_pk(a.dIt + ro, c, h);
+      w.civ = load_pk(a.ci + t * fs + ro, c, h);
+    }
+    return w;
+  };
+  // one row per wave: its tiles are loaded first, their latency overlaps the staging
+  BbRow<S> pre;
+  if constexpr (RPP == 1) pre = load_row(clip_off(b) + (size_t)(y0 + wave) * IMG * C);
   slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);        // i_w, i_u, e_w, e_u
-  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
+  stage_x(a.x, L.xs, b, t, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   gacc_zero(L.gacc, 4, tid);
   __syncthreads();
 
@@ -889,15 +917,25 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   const int slots[6] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B};
   float bs0 = 0.f, bs1 = 0.f;
 
-  if (!(a.ablate & 4)) {
+#pragma unroll 1
+  for (int i = 0; i < RPP && !(a.ablate & 4); ++i) {
+    const int yl = wave * RPP + i, y = y0 + yl;
+    const size_t ro = clip_off(b) + (size_t)y * IMG * C;
+    BbRow<S> w;
+    if constexpr (RPP == 1) w = pre;
+    else w = load_row(ro);
+    const Pk<S>& ginh = w.ginh;
+    const Pk<S>& dIt = w.dIt;
+    const Pk<S>& civ = w.civ;
+    Pk<S>& Iprev = w.Iprev;
     F pe[Tr<S>::KS];
     {
       f32x16 depf;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) depf[r] = (float)dep[r];
+      for (int r = 0; r < 16; ++r) depf[r] = (float)w.dep[r];
       if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
-      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, gEv, lane, wave, tid);
-      sm[3] = hsum16(depf);
+      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, w.gEv, lane, wave, tid);
+      sm[3] += hsum16(depf);
       cl_to_pa<S>(wscr, depf, lane, pe);
       const f32x16 dIt0 = a.no_inh ? load_cl(a.dIt + ro, c, h) : zero16();
       const f32x16 dg = gemm_pa<S>(pe, a.gt[5], dIt0, lane);   // no_inh: I_t = gE_t
@@ -978,6 +1016,45 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5
   if (!a.no_inh) gacc_flush(L.gacc, L.slabl, slab_p, 2, 2, tid);
   gacc_flush(L.gacc + 2 * 1024, L.slabl, slab_p, 4, 2, tid);
+}
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.ablate & 512) return;
+  pw_bb_body<S, ACT, HG, PWB_RPP>(a, smem, blockIdx.x / PWB_WGPC, blockIdx.x % PWB_WGPC);
+}
+
+// -------------------------------------------------------------------------
+// Fused backward frame steps: the point-wise work that consumes a conv's
+// output runs in the conv's own workgroup (one clip each), right after it,
+// with the LDS re-carved (no grid-wide dependency lies between them: only the
+// BatchNorm-backward sums, which the NEXT launch needs, cross clips).  Saves a
+// launch per step and the re-read of dI_t / dgE from HBM; the point-wise part
+// runs at one wave per SIMD with 8 rows per wave.
+//   k_conv_pw_bb(t): conv^T(BN1-bwd(dcE), w_exc) + adds -> dI_t, then pw_bb(t)
+//   k_conv_pw_ba(t): conv^T(BN0-bwd(dcI), w_inh) + dgEp -> dgE_t (t >= 1; at
+//                    t = 0 only the BN-bwd fill), then pw_ba(t - 1)
+// -------------------------------------------------------------------------
+constexpr int PWX_RPP = IMG / NWAVE;    // 8 rows per wave: the whole clip
+static_assert(NT == PW_NT, "fused kernels run the point-wise bodies with the conv workgroup");
+template <class S>
+constexpr int fused_lds_bytes() {
+  return conv_lds_bytes<S>() > pw_lds_bytes<PWX_RPP, true>() ? conv_lds_bytes<S>()
+                                                              : pw_lds_bytes<PWX_RPP, true>();
+}
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(NT, 1) void k_conv_pw_bb(ConvArgs<S> ca, CellArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_body<S, FILL_BNBWD, EPI_ADD>(ca, smem, blockIdx.x);
+  __syncthreads();              // dI_t stores visible to the workgroup; LDS free
+  pw_bb_body<S, ACT, HG, PWX_RPP>(a, smem, blockIdx.x, 0);
+}
+template <class S, int ACT, int HG, int EPI>
+__global__ __launch_bounds__(NT, 1) void k_conv_pw_ba(ConvArgs<S> ca, CellArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_body<S, FILL_BNBWD, EPI>(ca, smem, blockIdx.x);
+  __syncthreads();
+  pw_ba_body<S, ACT, HG, PWX_RPP>(a, smem, blockIdx.x, 0);
 }
 
 // D rows per band: 8 (bf16) / 4 (f32, so that two band buffers fit in LDS)
@@ -1143,23 +1220,62 @@ __device__ __forceinline__ void wgrad_band(f32x16 (&acc)[WG_NACC], const S* xt, 
   }
 }
 
-template <class S, int K>
-__device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __restrict__ Xs,
-                                          const S* __restrict__ Ds, int B, int T, int g, int nwg,
-                                          S* buf, int tid, int lane, int wave, int ablate, int ntx,
-                                          int nty) {
-  constexpr int KK = K * K;
-  const bool tiled = ntx * nty > 1;
-  // wave-uniform element offset of each tap; taps beyond K*K (the 13th slot of
-  // waves 1-3 at K=7) read tap 0 and their accumulator is never stored, so
-  // every MFMA is unconditional (no accumulator copies around branches)
-  int toff[WG_NACC];
+// bf16: tap-column blocking.  Wave w owns kernel columns kw0 = 2w, 2w + 1 (all
+// kh; 14 accumulator tiles, wave 3 only column 6 at K = 7).  The band's 16 B
+// fragments (8 D rows x 2 pixel blocks) are read once into registers; then for
+// every X row r of the band ONE A fragment per column feeds the MFMAs of all
+// taps kh with D row r - kh.  LDS reads per MFMA: 1/7 for A (was 1 with one
+// tap per A read) -- the old tap-scattered assignment was bound by the
+// transposing LDS reads.
+constexpr int WG2_NACC = 14;             // acc[j * 7 + kh]: tap (kh, kw0 + j)
+template <int K, int NKW>
+__device__ __forceinline__ void wgrad_band2(f32x16 (&acc)[WG2_NACC], const bf16_t* xt,
+                                            const bf16_t* dt, int kw0, int lane) {
+  constexpr int off = PADMAX - K / 2;
+  constexpr int RB = wg_rb<bf16_t>();
+  const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
+  const int chb = 16 * (grp & 1) + 4 * pp;
+  const int hh = grp >> 1;
+  bf16x8 bv[RB][2];
 #pragma unroll
-  for (int m = 0; m < WG_NACC; ++m) {
-    const int tap = wave + 4 * m < KK ? wave + 4 * m : 0;
-    const int kh = tap / K, kw = tap - kh * K;
-    toff[m] = (kh * TILE + kw) * C;
+  for (int yd = 0; yd < RB; ++yd)
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) bv[yd][blk] = tr_read8(dt + wd_off(yd, blk * 16 + 8 * hh + q, chb));
+  // steps st = (X row r, pixel block): A fragments read one step ahead; the
+  // sched_barriers keep the compiler from hoisting every read of the unrolled
+  // band to the top (which spilled)
+  constexpr int NST = (RB + K - 1) * 2;
+  auto xaddr = [&](int st) {
+    return xt + wx_off((st >> 1) + off, (st & 1) * 16 + 8 * hh + q + off + kw0, chb);
+  };
+  bf16x8 a0[2], a1[2];
+  a0[0] = tr_read8(xaddr(0));
+  if constexpr (NKW > 1) a1[0] = tr_read8(xaddr(0) + C);
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    const int r = st >> 1, blk = st & 1, cur = st & 1, nxt = cur ^ 1;
+    if (st + 1 < NST) {
+      a0[nxt] = tr_read8(xaddr(st + 1));
+      if constexpr (NKW > 1) a1[nxt] = tr_read8(xaddr(st + 1) + C);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+      const int yd = r - kh;
+      if (yd >= 0 && yd < RB) {
+        acc[kh] = Tr<bf16_t>::mma(a0[cur], bv[yd][blk], acc[kh]);
+        if constexpr (NKW > 1) acc[7 + kh] = Tr<bf16_t>::mma(a1[cur], bv[yd][blk], acc[7 + kh]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+template <class S, int K, class Body>
+__device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
+                                          const S* __restrict__ Ds, int B, int T, int g, int nwg,
+                                          S* buf, int tid, int ablate, int ntx, int nty) {
+  const bool tiled = ntx * nty > 1;
   constexpr int BE = wgrad_band_elems<S>();
   constexpr int NB = IMG / wg_rb<S>();                          // bands per (frame, clip)
   const int npairs = (B * T - g + nwg - 1) / nwg;
@@ -1180,7 +1296,7 @@ __device__ __forceinline__ void wgrad_run(f32x16 (&acc)[WG_NACC], const S* __res
     const bool more = u + 1 < nunits;
     if (more && !(ablate & 128))
       band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * wg_rb<S>(), tid, ntx, nty);
-    if (!(ablate & 64)) wgrad_band<S, K>(acc, xt, dt, toff, lane);
+    if (!(ablate & 64)) body(xt, dt);
     if (more) {
       S* xn = buf + ((u + 1) & 1) * BE;
       if (!(ablate & 128)) band.store(xn, xn + wg_xr<S>() * TILE * C, tid, tiled);
@@ -1207,24 +1323,69 @@ __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, in
   const S* Xs = conv == 0 ? a.gE : a.I;
   const S* Ds = conv == 0 ? a.dci_s : a.dce_s;
 
-  f32x16 acc[WG_NACC];
-#pragma unroll
-  for (int m = 0; m < WG_NACC; ++m) acc[m] = zero16();
-  switch (a.K) {
-    case 7: wgrad_run<S, 7>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
-    case 5: wgrad_run<S, 5>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
-    case 3: wgrad_run<S, 3>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
-    default: wgrad_run<S, 1>(acc, Xs, Ds, a.B, a.T, g, nwg, buf, tid, lane, wave, a.ablate, a.ntx, a.nty); break;
-  }
-  // acc[m]: rows ci = cl_x(r,h), cols n = lane&31
   float* dst = wslab + ((size_t)conv * nwg + g) * MAXTAP * 1024;
   const int n = lane & 31;
+  if constexpr (sizeof(S) == 2) {
+    f32x16 acc[WG2_NACC];
 #pragma unroll
-  for (int m = 0; m < WG_NACC; ++m) {
-    const int tap = wave + 4 * m;
-    if (tap < KK) {
+    for (int m = 0; m < WG2_NACC; ++m) acc[m] = zero16();
+    const int kw0 = 2 * wave;
+    auto run = [&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      // every wave runs two columns; a column kw >= K (wave 3's second at
+      // K = 7) reads in-bounds LDS and its tiles are never stored: uniform
+      // code, and that wave is otherwise idle while the others finish
+      wgrad_run<S, K>([&](const S* xt, const S* dt) { wgrad_band2<K, 2>(acc, xt, dt, kw0, lane); },
+                      Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
+    };
+    switch (a.K) {
+      case 7: run(std::integral_constant<int, 7>{}); break;
+      case 5: run(std::integral_constant<int, 5>{}); break;
+      case 3: run(std::integral_constant<int, 3>{}); break;
+      default: run(std::integral_constant<int, 1>{}); break;
+    }
+    // acc[j * 7 + kh]: rows ci = cl_x(r,h), cols n = lane&31
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dst[tap * 1024 + n * 32 + cl_x(r, h)] = acc[m][r];
+    for (int m = 0; m < WG2_NACC; ++m) {
+      const int kh = m % 7, kw = kw0 + m / 7;
+      if (kh < a.K && kw < a.K) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(kh * a.K + kw) * 1024 + n * 32 + cl_x(r, h)] = acc[m][r];
+      }
+    }
+  } else {
+    f32x16 acc[WG_NACC];
+#pragma unroll
+    for (int m = 0; m < WG_NACC; ++m) acc[m] = zero16();
+    // wave-uniform element offset of each tap; taps beyond K*K (the 13th slot
+    // of waves 1-3 at K=7) read tap 0 and their accumulator is never stored,
+    // so every MFMA is unconditional (no accumulator copies around branches)
+    auto run = [&](auto kc) {
+      constexpr int K = decltype(kc)::value;
+      int toff[WG_NACC];
+#pragma unroll
+      for (int m = 0; m < WG_NACC; ++m) {
+        const int tap = wave + 4 * m < K * K ? wave + 4 * m : 0;
+        const int kh = tap / K, kw = tap - kh * K;
+        toff[m] = (kh * TILE + kw) * C;
+      }
+      wgrad_run<S, K>([&](const S* xt, const S* dt) { wgrad_band<S, K>(acc, xt, dt, toff, lane); },
+                      Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
+    };
+    switch (a.K) {
+      case 7: run(std::integral_constant<int, 7>{}); break;
+      case 5: run(std::integral_constant<int, 5>{}); break;
+      case 3: run(std::integral_constant<int, 3>{}); break;
+      default: run(std::integral_constant<int, 1>{}); break;
+    }
+    // acc[m]: rows ci = cl_x(r,h), cols n = lane&31
+#pragma unroll
+    for (int m = 0; m < WG_NACC; ++m) {
+      const int tap = wave + 4 * m;
+      if (tap < KK) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[tap * 1024 + n * 32 + cl_x(r, h)] = acc[m][r];
+      }
     }
   }
 }
@@ -1435,6 +1596,7 @@ void timed(int kind, hipStream_t st, F&& launch) {
   g_tm.ev.emplace_back(a, b);
 }
 
+bool fused_enabled();
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
@@ -1556,6 +1718,18 @@ void launch_pw(K kern, dim3 grid, size_t lds, hipStream_t st, const A& a) {
           : (a.act ? launch_pw(kern<S, 1, 0>, grid, lds, st, a)                  \
                    : launch_pw(kern<S, 0, 0>, grid, lds, st, a)))
 
+// fused conv + point-wise kernels: (activation, cell) -> instantiation
+#define COMMA ,
+template <class K, class CA, class A>
+void launch_fused(K kern, int grid, size_t lds, hipStream_t st, const CA& ca, const A& a) {
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, ca, a);
+}
+#define FUSED_LAUNCH(kern, extra, cargs)                                              \
+  (a.hgru ? (a.act ? launch_fused(kern<S, 1, 1 extra>, p.B, lfu, st, cargs, a)        \
+                   : launch_fused(kern<S, 0, 1 extra>, p.B, lfu, st, cargs, a))       \
+          : (a.act ? launch_fused(kern<S, 1, 0 extra>, p.B, lfu, st, cargs, a)        \
+                   : launch_fused(kern<S, 0, 0 extra>, p.B, lfu, st, cargs, a)))
+
 #define SETLDS(kern, bytes) \
   HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
 
@@ -1583,6 +1757,12 @@ int set_lds_attrs() {
   SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
   SETLDS((k_pw_bb<S, 1, 1>), (pw_lds_bytes<PWB_RPP, true>()));
   SETLDS(k_wgrad<S>, wgrad_lds_bytes<S>());
+#define SETLDS_FUSED(A, H)                                                         \
+  SETLDS((k_conv_pw_bb<S, A, H>), fused_lds_bytes<S>());                           \
+  SETLDS((k_conv_pw_ba<S, A, H, EPI_ADD>), fused_lds_bytes<S>());                  \
+  SETLDS((k_conv_pw_ba<S, A, H, EPI_NONE>), fused_lds_bytes<S>());
+  SETLDS_FUSED(0, 0) SETLDS_FUSED(0, 1) SETLDS_FUSED(1, 0) SETLDS_FUSED(1, 1)
+#undef SETLDS_FUSED
   done = true;
   return 0;
 }
@@ -1662,7 +1842,31 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   a.t = p.T - 1;
   a.conv_done = 0;
   timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
-  for (int t = p.T - 1; t >= 0; --t) {
+  const bool fused = fused_enabled();
+  const size_t lfu = fused_lds_bytes<S>();
+  for (int t = p.T - 1; t >= 0 && fused; --t) {
+    ConvArgs<S> cb = conv_args(a);
+    cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
+    cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
+    cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
+    a.t = t;
+    timed(PT_K_BWD_C, st, [&] { FUSED_LAUNCH(k_conv_pw_bb, , cb); });
+    if (!d->no_inh) {
+      ConvArgs<S> ca = conv_args(a);
+      ca.dc = a.dcI; ca.raw = a.ci + t * fs; ca.bnstat = bst + (size_t)t * 128;
+      ca.bnb = a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64; ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
+      ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
+      a.t = t - 1;
+      a.conv_done = t >= 1;
+      if (t >= 1) timed(PT_K_BWD_D, st, [&] { FUSED_LAUNCH(k_conv_pw_ba, COMMA EPI_ADD, ca); });
+      else timed(PT_K_BWD_D, st, [&] { FUSED_LAUNCH(k_conv_pw_ba, COMMA EPI_NONE, ca); });
+    } else {
+      a.t = t - 1;
+      a.conv_done = 0;
+      timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+    }
+  }
+  for (int t = p.T - 1; t >= 0 && !fused; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
     cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
@@ -1717,6 +1921,16 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
 ptg::GraphCache g_graphs;
 bool use_graph() {
   return ptg::graphs_enabled() && __atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) == 0;
+}
+// PT_CELL_FUSED=1 selects the fused backward frame steps (k_conv_pw_bb /
+// k_conv_pw_ba).  Off by default: measured slower (B=256 T=64 bf16: 119.5 us
+// vs 42 + 66 us for conv_bb + pw_bb, 100 vs 37 + 55 us for conv_ba + pw_ba,
+// 10.0k vs 10.9k clips/s) -- the point-wise half at one wave per SIMD with 8
+// rows per wave exposes its VALU and memory latency that 2 workgroups per CU
+// hide in the separate launches.
+bool fused_enabled() {
+  const char* f = getenv("PT_CELL_FUSED");
+  return f && atoi(f) != 0;
 }
 int ablate_env() {
   const char* ab = getenv("PT_CELL_ABLATE");
@@ -1783,7 +1997,8 @@ int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params
   if (!use_graph()) return body(st);
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
-  k.add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env());
+  k.add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
+      .add((int)fused_enabled());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 

@@ -134,6 +134,20 @@ __device__ __forceinline__ void store_pl(bf16_t* __restrict__ px, int h, const f
     *(bf16x4*)(px + 8 * g + 4 * h) = bf16x4{(bf16_t)v[4 * g], (bf16_t)v[4 * g + 1],
                                             (bf16_t)v[4 * g + 2], (bf16_t)v[4 * g + 3]};
 }
+// Streaming (nontemporal) form of store_pl for outputs written once per launch.
+__device__ __forceinline__ void store_pl_nt(float* __restrict__ px, int h, const f32x16& v) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    __builtin_nontemporal_store(f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]},
+                                (f32x4*)(px + 8 * g + 4 * h));
+}
+__device__ __forceinline__ void store_pl_nt(bf16_t* __restrict__ px, int h, const f32x16& v) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    __builtin_nontemporal_store(bf16x4{(bf16_t)v[4 * g], (bf16_t)v[4 * g + 1], (bf16_t)v[4 * g + 2],
+                                       (bf16_t)v[4 * g + 3]},
+                                (bf16x4*)(px + 8 * g + 4 * h));
+}
 __device__ __forceinline__ void add_pl(const float* __restrict__ px, int h, f32x16& v) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
