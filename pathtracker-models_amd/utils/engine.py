@@ -11,9 +11,12 @@ runs unchanged.  Differences, all deliberate:
   value mapping goes through a 256-entry table built as ``float32(u / 255.)``
   in float64, i.e. exactly the reference's numpy arithmetic, so the result is
   bit-identical.
-* Models outside the hot path (torchvision / slowfast / transformer / kys /
-  hGRU-SEG baselines) are out of scope here and raise ``NotImplementedError``
-  with the reference's own message.
+* The comparison baselines 'gru' (models/kys.py) and 'nostride_video_cc_small'
+  (models/nostridetv_cc_smallest.py) are stock-PyTorch modules; the other
+  feedforward baselines (torchvision r3d/mc3/r2plus1 with hub weights,
+  slowfast, transformer / performer / lambda wrappers, TSM) depend on
+  packages or downloads absent offline and raise ``NotImplementedError`` with
+  the reference's own message, as does the absent hGRU-SEG module.
 """
 import os
 
@@ -23,6 +26,8 @@ import torch.nn.functional as F
 
 from models import InT
 from models import ffhgru_hierarchy
+from models import kys
+from models import nostridetv_cc_smallest
 
 TORCHVISION = ['r3d', 'mc3', 'r2plus1', 'nostride_r3d', 'nostride_r3d_pos']
 SLOWFAST = ['slowfast', 'slowfast_nl']
@@ -70,6 +75,12 @@ def model_selector(args, timesteps, device, fb_kernel_size=7, dimensions=32):
     'ffhgru' (not registered by the reference's engine, whose 'hgru' entry
     imports the absent models/hgrucleanSEG.py) builds
     models/ffhgru_hierarchy.py's FFhGRU."""
+    if args.model == 'gru':                      # engine.py:147-153 (comparison baseline)
+        return kys.GRU(dimensions=dimensions * 2, timesteps=timesteps, kernel_size=fb_kernel_size,
+                       jacobian_penalty=False, grad_method='bptt')
+    if args.model == 'nostride_video_cc_small':  # engine.py:204-206 (comparison baseline)
+        return nostridetv_cc_smallest.r3d_18(pretrained=getattr(args, 'pretrained', False),
+                                             timesteps=timesteps)
     if args.model == 'ffhgru':
         return ffhgru_hierarchy.FFhGRU(dimensions=dimensions, timesteps=timesteps,
                                        kernel_size=fb_kernel_size, jacobian_penalty=False,

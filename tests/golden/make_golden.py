@@ -149,6 +149,57 @@ def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0, want_gates=True, hw=
     print(tag, "loss", float(out["loss"]))
 
 
+def make_gru(ref_kys, tag, *, batch, t_len, dims, seed=0):
+    """kys.GRU comparison baseline (models/kys.py:70-135): init under a seed,
+    then testmode / training outputs, grads and one Adam step."""
+    synth = _synth()
+    torch.manual_seed(3000 + seed)
+    model = ref_kys.GRU(dimensions=dims, timesteps=t_len, kernel_size=7)
+    init = {"init." + k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    clips, labels = synth.make_batch(seed + 20, batch, t_len)
+    x, y = prepare(clips, labels)
+    out = run_recurrent(model, x, y, want_gates=True)
+    out.update(init)
+    out.update(clip_u8=clips, label_u8=np.array([ord(b) for b in labels], np.uint8),
+               cfg_dims=np.array(dims), cfg_seed=np.array(3000 + seed))
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
+    print(tag, "loss", float(out["loss"]))
+
+
+def make_r3d(ref_r3d, tag, *, batch, t_len, seed=0):
+    """nostridetv_cc_smallest.r3d_18 comparison baseline: init under a seed,
+    eval logits (running stats), training logits / loss / grads (batch stats),
+    the running stats after that step, one Adam step."""
+    synth = _synth()
+    torch.manual_seed(4000 + seed)
+    model = ref_r3d.r3d_18(timesteps=t_len)
+    out = {"init." + k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    clips, labels = synth.make_batch(seed + 30, batch, t_len)
+    x, y = prepare(clips, labels)
+    model.eval()
+    with torch.no_grad():
+        out["logits"] = model(x)[0].numpy()
+    model.train()
+    logits, _ = model(x)
+    loss = F.binary_cross_entropy_with_logits(logits, y.reshape(-1, 1))
+    loss.backward()
+    out["train_logits"] = logits.detach().numpy()
+    out["loss"] = np.array(loss.item(), dtype=np.float32)
+    for name, p in model.named_parameters():
+        out["grad." + name] = p.grad.numpy().copy()
+    for k, v in model.state_dict().items():
+        if "running" in k:
+            out["after." + k] = v.numpy().copy()
+    opt = torch.optim.Adam(model.parameters(), lr=3e-4)
+    opt.step()
+    for name, p in model.named_parameters():
+        out["adam." + name] = p.detach().numpy().copy()
+    out.update(clip_u8=clips, label_u8=np.array([ord(b) for b in labels], np.uint8),
+               cfg_seed=np.array(4000 + seed))
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
+    print(tag, "loss", float(out["loss"]))
+
+
 def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0):
     torch.manual_seed(3000 + seed)
     cwd = os.getcwd()
@@ -232,6 +283,8 @@ def main():
         ref_int.FFhGRU = ref_int.InT
         ref_hgru = _load("ref_ffhgru", os.path.join(REF, "models", "ffhgru_hierarchy.py"))
         ref_clstm = _load("ref_convlstm", os.path.join(REF, "models", "convlstm.py"))
+        ref_kys = _load("ref_kys", os.path.join(REF, "models", "kys.py"))
+        ref_r3d = _load("ref_r3d", os.path.join(REF, "models", "nostridetv_cc_smallest.py"))
 
         jobs = {
             "init_seed123": lambda: make_init(ref_int, "init_seed123"),
@@ -255,6 +308,9 @@ def main():
                                          seed=11, hw=(64, 64)),
             "int_64x96": lambda: make_int(ref_int, "int_64x96", batch=2, t_len=3, dims=32,
                                           seed=12, hw=(64, 96)),
+            # feedforward / recurrent comparison baselines (BASELINE configs[4])
+            "gru_c16": lambda: make_gru(ref_kys, "gru_c16", batch=2, t_len=4, dims=16, seed=1),
+            "r3d_small": lambda: make_r3d(ref_r3d, "r3d_small", batch=2, t_len=4, seed=2),
             "init_convlstm_seed123": lambda: make_init_convlstm(ref_clstm, "init_convlstm_seed123"),
             "convlstm_k7": lambda: make_convlstm(ref_clstm, "convlstm_k7", batch=2, timesteps=4,
                                                  filt=7, seed=7),
