@@ -271,6 +271,17 @@ constexpr int CONV_MISC = 512;  // floats: red[256] (bn-bwd table [3][32] aliase
 template <class S>
 constexpr int conv_lds_bytes() { return tile_bytes<S>() + CONV_MISC * 4 + 2 * WSLICE_BYTES; }
 
+// conv_run row hook of EPI_FWD: store a finished output row (PL layout)
+template <class S>
+struct StoreRow {
+  S* base;
+  int h;
+  static constexpr bool active = true;
+  __device__ __forceinline__ void operator()(int i, const f32x16& v) const {
+    store_pl(base + (size_t)i * IMG * C, h, v);
+  }
+};
+
 template <class S, int FILL, int EPI>
 __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b) {
   S* tile = (S*)smem;
@@ -372,18 +383,17 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
     f32x16 acc[RPW];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) acc[i] = zero16();
-    conv_run<S>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate);
-    if (a.ablate & 256) return;
     const int px = lane & 31;
     if constexpr (EPI == EPI_FWD) {
-#pragma unroll
-      for (int i = 0; i < RPW; ++i) {
-        if (a.ablate & 2048) continue;
-        if (a.ablate & 1024) store_pl_nt(a.out_raw + cb + ((size_t)(wave * RPW + i) * IMG + px) * C, h, acc[i]);
-        else store_pl(a.out_raw + cb + ((size_t)(wave * RPW + i) * IMG + px) * C, h, acc[i]);
-      }
+      // each finished row is stored while the later rows' MFMAs still run
+      // (all 256 workgroups storing at the very end took ~6.5 us per launch)
+      const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RPW) * IMG + px) * C, h};
+      conv_run<S>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate, sr);
+      if (a.ablate & 256) return;
       if (!(a.ablate & 8)) bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
     } else {
+      conv_run<S>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate);
+      if (a.ablate & 256) return;
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         const size_t po = cb + ((size_t)(wave * RPW + i) * IMG + px) * C;

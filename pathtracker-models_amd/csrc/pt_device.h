@@ -442,10 +442,19 @@ __device__ __forceinline__ void wslice_store(WSlice& r, char* buf, int tid) {
   if (tid + 3 * NT < WSLICE_CHUNKS) b[tid + 3 * NT] = r.v3;
 }
 
-template <class S, int K, class Fill>
+// Row-final hook: called as done(i, acc[i]) the moment output row i has
+// received its last MFMA (last pass, last kernel column, tile row i + K - 1),
+// so an epilogue can store row i while the later rows' MFMAs still run.
+struct NoRowHook {
+  __device__ __forceinline__ void operator()(int, const f32x16&) const {}
+  static constexpr bool active = false;
+};
+
+template <class S, int K, class Fill, class Done = NoRowHook>
 __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
                                            const typename Tr<S>::frag* __restrict__ wf, S* tile,
-                                           char* wbuf, int row0, int lane, int tid, int ablate) {
+                                           char* wbuf, int row0, int lane, int tid, int ablate,
+                                           const Done& done = Done()) {
   using TT = Tr<S>;
   using F = typename TT::frag;
   constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
@@ -500,6 +509,10 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (Done::active) {
+          const int i = tr - (K - 1);
+          if (i >= 0 && i < RPW && kw == K - 1 && pass == TT::NPASS - 1) done(i, acc[i < 0 ? 0 : i]);
+        }
       }
       if (kw + 1 < K) {
         wslice_store<K>(pre, wbuf + ((kw + 1) & 1) * WSLICE_BYTES, tid);
@@ -509,16 +522,16 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
   }
 }
 
-template <class S, class Fill>
+template <class S, class Fill, class Done = NoRowHook>
 __device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], Fill& fill,
                                          const typename Tr<S>::frag* __restrict__ wf, S* tile,
                                          char* wbuf, int K, int row0, int lane, int tid,
-                                         int ablate) {
+                                         int ablate, const Done& done = Done()) {
   switch (K) {
-    case 7: conv_run_k<S, 7>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
-    case 5: conv_run_k<S, 5>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
-    case 3: conv_run_k<S, 3>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
-    default: conv_run_k<S, 1>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate); break;
+    case 7: conv_run_k<S, 7>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+    case 5: conv_run_k<S, 5>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+    case 3: conv_run_k<S, 3>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+    default: conv_run_k<S, 1>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
   }
 }
 
