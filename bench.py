@@ -274,6 +274,8 @@ def main():
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
             "loss": round(float(loss.item()), 5),
         }
+        if not np.isfinite(line["loss"]):
+            print("bench.py: WARNING non-finite training loss", file=sys.stderr, flush=True)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, frames=args.frames)
         print(json.dumps(line), flush=True)

@@ -7,6 +7,7 @@
 // caller-owned batch buffers.  See include/pt_tfrecord.h.
 #include "../../include/pt_tfrecord.h"
 
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -235,7 +236,96 @@ struct FileResult {
   bool done = false;
 };
 
+// ---------------------------------------------------- libdeflate fast path
+// The system's libdeflate (runtime library only, no header in the image) is
+// ~2-3x faster than zlib at inflating whole gzip members; resolved with dlopen
+// at first use, zlib is the fallback.  Its stable C API (libdeflate.h):
+struct libdeflate_decompressor;
+typedef libdeflate_decompressor* (*ld_alloc_t)(void);
+typedef int (*ld_gzip_ex_t)(libdeflate_decompressor*, const void* in, size_t in_nbytes, void* out,
+                            size_t out_nbytes_avail, size_t* actual_in_nbytes_ret,
+                            size_t* actual_out_nbytes_ret);
+typedef void (*ld_free_t)(libdeflate_decompressor*);
+struct LibDeflate {
+  ld_alloc_t alloc = nullptr;
+  ld_gzip_ex_t gzip_ex = nullptr;
+  ld_free_t free_ = nullptr;
+  LibDeflate() {
+    const char* off = getenv("PT_TFR_ZLIB_ONLY");
+    if (off && atoi(off)) return;
+    void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    alloc = (ld_alloc_t)dlsym(h, "libdeflate_alloc_decompressor");
+    gzip_ex = (ld_gzip_ex_t)dlsym(h, "libdeflate_gzip_decompress_ex");
+    free_ = (ld_free_t)dlsym(h, "libdeflate_free_decompressor");
+    if (!alloc || !gzip_ex || !free_) alloc = nullptr;
+  }
+  bool ok() const { return alloc != nullptr; }
+};
+const LibDeflate& libdeflate() {
+  static const LibDeflate ld;
+  return ld;
+}
+
+// Whole file -> memory; gzip members inflated by libdeflate.  Returns 1 if the
+// fast path is unavailable (caller falls back to zlib), 0 on success, < 0 on error.
+int read_all_libdeflate(const std::string& path, std::vector<uint8_t>& out, std::string& msg) {
+  const LibDeflate& ld = libdeflate();
+  if (!ld.ok()) return 1;
+  FILE* fp = fopen(path.c_str(), "rb");
+  if (!fp) {
+    msg = "cannot open " + path;
+    return PT_TFR_ERR_IO;
+  }
+  std::vector<uint8_t> in;
+  if (fseek(fp, 0, SEEK_END) == 0) {
+    const long sz = ftell(fp);
+    if (sz > 0) in.resize((size_t)sz);
+    fseek(fp, 0, SEEK_SET);
+  }
+  const size_t got = in.empty() ? 0 : fread(in.data(), 1, in.size(), fp);
+  fclose(fp);
+  if (got != in.size()) {
+    msg = "short read on " + path;
+    return PT_TFR_ERR_IO;
+  }
+  if (in.size() < 18 || in[0] != 0x1f || in[1] != 0x8b) {      // not gzip: the file as is
+    out.swap(in);
+    return 0;
+  }
+  libdeflate_decompressor* d = ld.alloc();
+  if (!d) return 1;
+  // output estimate: the last member's ISIZE, grown on demand
+  const uint8_t* t = in.data() + in.size() - 4;
+  size_t cap = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+  if (cap < (1u << 20)) cap = 1u << 20;
+  out.resize(cap);
+  size_t ipos = 0, opos = 0;
+  int rc = 0;
+  while (ipos < in.size()) {                   // concatenated members
+    size_t in_used = 0, out_len = 0;
+    const int r = ld.gzip_ex(d, in.data() + ipos, in.size() - ipos, out.data() + opos,
+                             out.size() - opos, &in_used, &out_len);
+    if (r == 3) {                              // LIBDEFLATE_INSUFFICIENT_SPACE
+      out.resize(out.size() * 2);
+      continue;
+    }
+    if (r != 0) {
+      msg = "gzip error in " + path + " (libdeflate " + std::to_string(r) + ")";
+      rc = PT_TFR_ERR_FORMAT;
+      break;
+    }
+    ipos += in_used;
+    opos += out_len;
+  }
+  ld.free_(d);
+  if (rc) return rc;
+  out.resize(opos);
+  return 0;
+}
+
 int read_all(const std::string& path, std::vector<uint8_t>& out, std::string& msg) {
+  if (int rc = read_all_libdeflate(path, out, msg); rc <= 0) return rc;
   gzFile f = gzopen(path.c_str(), "rb");       // transparently reads plain files too
   if (!f) {
     msg = "cannot open " + path;

@@ -90,13 +90,15 @@ def validate(args, val_loader, model, criterion, device, results_folder, len_val
 
 def write_synthetic(root, n_clips, length, rank, world, seed=0):
     """Seeded synthetic PathTracker shards (ptamd/synth.py) as GZIP TFRecords:
-    train-* and test-*, at least one shard per rank."""
+    train-* and test-*, 16 shards per split (a multiple of the rank count),
+    so that every rank's reader has several files to decode in parallel."""
     from ptamd import tfrecord
     if rank == 0:
         os.makedirs(root, exist_ok=True)
-        per = max(1, n_clips // max(world, 1))
+        shards = max(world, 1) * max(1, 16 // max(world, 1))
+        per = max(1, n_clips // shards)
         for split, s in (("train", seed), ("test", seed + 1)):
-            tfrecord.write_synthetic_shards(root, max(world, 1), per, length, seed=s, prefix=split)
+            tfrecord.write_synthetic_shards(root, shards, per, length, seed=s, prefix=split)
     if world > 1:
         dist.barrier()
 

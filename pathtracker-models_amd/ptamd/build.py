@@ -54,7 +54,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         out = _out(lib)
         if srcs[0].endswith(".cpp"):
             cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared",
-                   "-pthread", "-Wall", "-I", INC, "-o", out + ".tmp", *srcs, "-lz"]
+                   "-pthread", "-Wall", "-I", INC, "-o", out + ".tmp", *srcs, "-lz", "-ldl"]
         else:
             cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                    "-I", INC, "-o", out + ".tmp", *srcs]

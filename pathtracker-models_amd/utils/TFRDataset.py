@@ -21,6 +21,8 @@ rank reads disjoint shards with no scatter.
 """
 import glob
 import os
+import queue
+import threading
 
 import numpy as np
 
@@ -57,31 +59,108 @@ def read_tfrecord(example, timesteps=64):
 
 
 class _Loader:
-    def __init__(self, files, batch_size, drop_remainder, shuffle_buffer, timesteps, seed):
+    """One pass = one native Reader.  Batches are produced by a background
+    thread (the native calls release the GIL) ``prefetch`` batches ahead, so
+    decoding and the copy into (optionally pinned) host memory overlap the
+    training step, as tf.data's pipeline does for the reference."""
+
+    def __init__(self, files, batch_size, drop_remainder, shuffle_buffer, timesteps, seed,
+                 prefetch=2, pin_memory=None):
         self.files, self.batch_size = files, batch_size
         self.drop_remainder, self.shuffle_buffer = drop_remainder, shuffle_buffer
         self.timesteps, self.seed, self.epoch = timesteps, seed, 0
+        self.prefetch = prefetch
+        self.pin_memory = pin_memory
+
+    def _batches(self, rd):
+        pin = self.pin_memory
+        if pin is None:
+            try:
+                import torch
+                pin = torch.cuda.is_available()
+            except ImportError:
+                pin = False
+        if not pin:
+            for clips, labels in rd.batches(self.batch_size):
+                yield _as_batch(clips), _as_batch(np.array([bytes([v]) for v in labels], dtype=object))
+            return
+        # pinned ring, filled in place by the native reader (pinning per batch
+        # costs more than decoding it).  A slot is refilled prefetch + 1 batches
+        # after it was handed out; engine.prepare_data copies it to the device
+        # synchronously, so the consumer is done with it by then.
+        import torch
+        ring = [torch.empty((self.batch_size,) + rd.shape, dtype=torch.uint8).pin_memory()
+                for _ in range(self.prefetch + 2)]
+        labs = [np.empty(self.batch_size, np.uint8) for _ in ring]
+        k = 0
+        while True:
+            got = rd.next(self.batch_size, (ring[k].numpy(), labs[k]))
+            if got is None:
+                return
+            n = len(got[1])
+            yield ring[k][:n], _as_batch(np.array([bytes([v]) for v in labs[k][:n]], dtype=object))
+            k = (k + 1) % len(ring)
 
     def __iter__(self):
         # reshuffle_each_iteration=True: a new shuffle seed per pass (:50)
         rank, world = _rank_world()
         rd = tfrecord.Reader(self.files, self.timesteps, rank=rank, world=world,
                              shuffle_buffer=self.shuffle_buffer, seed=self.seed + self.epoch,
-                             threads=min(8, max(1, len(self.files))),
+                             threads=min(16, os.cpu_count() or 1, max(1, len(self.files))),
                              drop_remainder=self.drop_remainder)
         self.epoch += 1
+        if self.prefetch <= 0:
+            try:
+                yield from self._batches(rd)
+            finally:
+                rd.close()
+            return
+        q = queue.Queue(maxsize=self.prefetch)
+        stop = threading.Event()
+        end = object()
+
+        def produce():
+            try:
+                for item in self._batches(rd):
+                    while not stop.is_set():
+                        try:
+                            q.put(item, timeout=0.1)
+                            break
+                        except queue.Full:
+                            continue
+                    if stop.is_set():
+                        return
+                q.put(end)
+            except BaseException as e:          # surfaced in the consumer
+                q.put(e)
+
+        th = threading.Thread(target=produce, daemon=True)
+        th.start()
         try:
-            for clips, labels in rd.batches(self.batch_size):
-                yield _as_batch(clips), _as_batch(np.array([bytes([v]) for v in labels], dtype=object))
+            while True:
+                item = q.get()
+                if item is end:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
         finally:
+            stop.set()
+            while th.is_alive():                # unblock a producer waiting on a full queue
+                try:
+                    q.get(timeout=0.05)
+                except queue.Empty:
+                    pass
+            th.join()
             rd.close()
 
 
 def tfr_data_loader(data_dir="", batch_size=32, drop_remainder=True, shuffle_buffer=1000,
-                    timesteps=64, seed=0):
+                    timesteps=64, seed=0, prefetch=2, pin_memory=None):
     """Iterable of ``(images [B,T,32,32,3] uint8, labels [B] 1-byte strings)``
     (reference utils/TFRDataset.py:31-53)."""
     if data_dir is None:
         raise ValueError("Missing path to data directory!")
     files = sorted(glob.glob(data_dir))
-    return _Loader(files, batch_size, drop_remainder, shuffle_buffer, timesteps, seed)
+    return _Loader(files, batch_size, drop_remainder, shuffle_buffer, timesteps, seed,
+                   prefetch=prefetch, pin_memory=pin_memory)

@@ -115,7 +115,7 @@ def prepare_data(imgs, target, args, device, disentangle_channels, use_augmentat
         raise NotImplementedError("use_augmentations: the reference's transform is undefined there")
     device = torch.device(device)
     u8 = imgs if isinstance(imgs, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(imgs))
-    u8 = u8.to(device, non_blocking=True)
+    u8 = u8.to(device)       # synchronous: the loader reuses its pinned host buffers
     if not disentangle_channels:
         x = _u8_to_unit(device)[u8.long()].permute(0, 4, 1, 2, 3).contiguous()
     else:

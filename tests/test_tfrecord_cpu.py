@@ -164,3 +164,28 @@ def test_loader_feeds_prepare_data(tmp_path):
     np.testing.assert_array_equal(x.numpy(), xr)
     np.testing.assert_array_equal(y.numpy(), yr)
     assert len(list(loader)) == 2                        # a second epoch re-reads
+
+
+def test_loader_prefetch_thread(tmp_path):
+    """The background producer yields the same batches as the synchronous path,
+    stops cleanly when the consumer breaks early, and re-raises reader errors."""
+    import threading
+    from utils.TFRDataset import tfr_data_loader
+    tfrecord.write_synthetic_shards(str(tmp_path), n_shards=3, clips_per_shard=6, timesteps=T)
+    pat = str(tmp_path / "*.tfrecord.gz")
+    sync = [b[0].copy() for b in tfr_data_loader(pat, 4, shuffle_buffer=0, timesteps=T, prefetch=0)]
+    pre = [np.asarray(b[0]).copy() for b in tfr_data_loader(pat, 4, shuffle_buffer=0, timesteps=T,
+                                                            prefetch=2, pin_memory=False)]
+    assert len(sync) == len(pre) == 4
+    for a, b in zip(sync, pre):
+        np.testing.assert_array_equal(a, b)
+    before = threading.active_count()
+    for i, _ in enumerate(tfr_data_loader(pat, 2, shuffle_buffer=0, timesteps=T, prefetch=1)):
+        if i == 1:
+            break                                          # generator closed mid-epoch
+    assert threading.active_count() <= before
+    bad = tmp_path / "bad"
+    bad.mkdir()
+    (bad / "x.tfrecord.gz").write_bytes(gzip.compress(b"\x05\x00\x00\x00\x00\x00\x00\x00junk"))
+    with pytest.raises(tfrecord.TFRecordError):
+        list(tfr_data_loader(str(bad / "*.gz"), 1, timesteps=T, prefetch=2, pin_memory=False))
