@@ -1803,7 +1803,7 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   }
   pa.wf_inh = (S*)((char*)saved + p.o_wf[0]); pa.wf_exc = (S*)((char*)saved + p.o_wf[1]);
   pa.wt_inh = (S*)((char*)saved + p.o_wf[2]); pa.wt_exc = (S*)((char*)saved + p.o_wf[3]);
-  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnacc, 0, (size_t)p.T * 2 * NBNC * 96 * 8, st));
+  HIPCHK(zero_async((char*)ws + p.o_bnacc, (size_t)p.T * 2 * NBNC * 96 * 8, st));
   timed(PT_K_PREP, st, [&] { hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa); });
   const dim3 gpf(p.B * PWF_WGPC);
   const size_t lpf = (pw_lds_bytes<PWF_RPP, false>()), lcv = conv_lds_bytes<S>();
@@ -1840,8 +1840,8 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   if (int rc = set_lds_attrs<S>()) return rc;
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
-  HIPCHK(hipMemsetAsync((char*)ws + p.o_slab, 0, (size_t)p.B * PW_PARTS * SLAB * 4, st));
-  HIPCHK(hipMemsetAsync((char*)ws + p.o_bnbacc, 0, (size_t)p.T * 2 * NBNC * 64 * 8, st));
+  HIPCHK(zero_async((char*)ws + p.o_slab, (size_t)p.B * PW_PARTS * SLAB * 4, st));
+  HIPCHK(zero_async((char*)ws + p.o_bnbacc, (size_t)p.T * 2 * NBNC * 64 * 8, st));
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
@@ -1907,7 +1907,7 @@ int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr
   }
   float* wslab = (float*)((char*)ws + p.o_wslab);
   const int conv0 = d->no_inh ? 1 : 0;
-  if (d->no_inh) HIPCHK(hipMemsetAsync(wslab, 0, (size_t)p.nwg * MAXTAP * 1024 * 4, st));
+  if (d->no_inh) HIPCHK(zero_async(wslab, (size_t)p.nwg * MAXTAP * 1024 * 4, st));
   timed(PT_K_WGRAD, st, [&] {
     hipLaunchKernelGGL(k_wgrad<S>, dim3(p.nwg, 2 - conv0), dim3(NT), wgrad_lds_bytes<S>(), st, a,
                        wslab, p.nwg, conv0); });

@@ -535,4 +535,26 @@ __device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], Fill& fill,
   }
 }
 
+// Zero-fill as a kernel node.  The captured launch sequences used
+// hipMemsetAsync; replayed as part of a hipGraph, the 54 MB slab clear was
+// not reliably ordered before the kernels that accumulate into the slab
+// (tools/nan_hunt.py: non-finite slab-derived gradients on some replays of
+// a cached graph, never with direct launches).
+__global__ void k_zero(uint32_t* __restrict__ p, size_t n_words) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t n16 = n_words / 4;
+  for (size_t j = i; j < n16; j += stride) ((u32x4*)p)[j] = u32x4{0u, 0u, 0u, 0u};
+  for (size_t j = n16 * 4 + i; j < n_words; j += stride) p[j] = 0u;
+}
+inline hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
+  // every cleared region is a multiple of 4 bytes and 16-byte aligned (256-B plan offsets)
+  const size_t words = bytes / 4;
+  size_t blocks = (words / 4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_zero, dim3((unsigned)blocks), dim3(256), 0, st, (uint32_t*)p, words);
+  return hipGetLastError();
+}
+
 }  // namespace ptc

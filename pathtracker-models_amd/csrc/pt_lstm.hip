@@ -863,7 +863,7 @@ int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
   if (d_c)
     hipLaunchKernelGGL(k_to_cl<float>, grid_for(p.npix * HC), dim3(256), 0, st, d_c, dc, p.B, p.ch);
   else
-    HIPCHK(hipMemsetAsync(dc, 0, p.npix * HC * 4, st));
+    HIPCHK(zero_async(dc, p.npix * HC * 4, st));
   HIPCHK(hipGetLastError());
   const bool want_dh0 = has_h0 && g->d_h0;
   for (int t = p.T - 1; t >= 0; --t) {

@@ -112,8 +112,12 @@ def main(argv=None):
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
+        # the host does little besides launching: keep PyTorch's (spinning)
+        # intra-op CPU pool small so the TFRecord decoder threads get the cores
+        torch.set_num_threads(2)
     else:
         device = torch.device("cpu")       # the cell itself raises: there is no CPU path
+    sys.setswitchinterval(5e-4)     # the loader thread's GIL hand-offs wait at most 0.5 ms
     if world > 1:
         dist.init_process_group("nccl" if device.type == "cuda" else "gloo")
     stem = "{}_{}_{}".format(args.length, args.speed, args.dist)

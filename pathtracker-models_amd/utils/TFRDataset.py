@@ -50,6 +50,11 @@ def _rank_world():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
 
+def _labels(codes):
+    """uint8 label codes -> the 1-byte strings a TF string tensor yields."""
+    return _as_batch(np.array([bytes([v]) for v in codes], dtype=object))
+
+
 def read_tfrecord(example, timesteps=64):
     """Parse one serialized Example (reference utils/TFRDataset.py:6-28)."""
     if hasattr(example, "numpy"):
@@ -61,11 +66,13 @@ def read_tfrecord(example, timesteps=64):
 class _Loader:
     """One pass = one native Reader.  Batches are produced by a background
     thread (the native calls release the GIL) ``prefetch`` batches ahead, so
-    decoding and the copy into (optionally pinned) host memory overlap the
-    training step, as tf.data's pipeline does for the reference."""
+    decoding overlaps the training step, as tf.data's pipeline does for the
+    reference.  The clip arrays live in a ring of ``prefetch + 2`` host
+    buffers: a batch stays valid until ``prefetch + 1`` further batches have
+    been taken (engine.prepare_data copies it to the device right away)."""
 
     def __init__(self, files, batch_size, drop_remainder, shuffle_buffer, timesteps, seed,
-                 prefetch=2, pin_memory=None):
+                 prefetch=2, pin_memory=False):
         self.files, self.batch_size = files, batch_size
         self.drop_remainder, self.shuffle_buffer = drop_remainder, shuffle_buffer
         self.timesteps, self.seed, self.epoch = timesteps, seed, 0
@@ -73,17 +80,27 @@ class _Loader:
         self.pin_memory = pin_memory
 
     def _batches(self, rd):
-        pin = self.pin_memory
-        if pin is None:
-            try:
-                import torch
-                pin = torch.cuda.is_available()
-            except ImportError:
-                pin = False
-        if not pin:
-            for clips, labels in rd.batches(self.batch_size):
-                yield _as_batch(clips), _as_batch(np.array([bytes([v]) for v in labels], dtype=object))
-            return
+        # pinned host memory from torch on ROCm is host-coherent: the reader's
+        # writes into it ran at 2.2k clips/s on the GPU box vs 20k clips/s into
+        # pageable memory (whose H2D copy in prepare_data takes ~3 ms per
+        # 50 MB batch), so pinning is opt-in
+        if not self.pin_memory:
+            if self.prefetch <= 0:
+                for clips, labels in rd.batches(self.batch_size):
+                    yield _as_batch(clips), labels
+                return
+            # host ring filled in place: one native call (GIL released) per
+            # batch and no 50 MB allocation -- a producer that needs the GIL
+            # often waits out the training loop's switch interval each time
+            ring = [np.empty((self.batch_size,) + rd.shape, np.uint8) for _ in range(self.prefetch + 2)]
+            labs = [np.empty(self.batch_size, np.uint8) for _ in ring]
+            k = 0
+            while True:
+                got = rd.next(self.batch_size, (ring[k], labs[k]))
+                if got is None:
+                    return
+                yield _as_batch(got[0]), got[1]
+                k = (k + 1) % len(ring)
         # pinned ring, filled in place by the native reader (pinning per batch
         # costs more than decoding it).  A slot is refilled prefetch + 1 batches
         # after it was handed out; engine.prepare_data copies it to the device
@@ -98,7 +115,7 @@ class _Loader:
             if got is None:
                 return
             n = len(got[1])
-            yield ring[k][:n], _as_batch(np.array([bytes([v]) for v in labs[k][:n]], dtype=object))
+            yield ring[k][:n], labs[k][:n]
             k = (k + 1) % len(ring)
 
     def __iter__(self):
@@ -111,7 +128,8 @@ class _Loader:
         self.epoch += 1
         if self.prefetch <= 0:
             try:
-                yield from self._batches(rd)
+                for clips, labels in self._batches(rd):
+                    yield clips, _labels(labels)
             finally:
                 rd.close()
             return
@@ -143,7 +161,7 @@ class _Loader:
                     return
                 if isinstance(item, BaseException):
                     raise item
-                yield item
+                yield item[0], _labels(item[1])
         finally:
             stop.set()
             while th.is_alive():                # unblock a producer waiting on a full queue
@@ -156,7 +174,7 @@ class _Loader:
 
 
 def tfr_data_loader(data_dir="", batch_size=32, drop_remainder=True, shuffle_buffer=1000,
-                    timesteps=64, seed=0, prefetch=2, pin_memory=None):
+                    timesteps=64, seed=0, prefetch=2, pin_memory=False):
     """Iterable of ``(images [B,T,32,32,3] uint8, labels [B] 1-byte strings)``
     (reference utils/TFRDataset.py:31-53)."""
     if data_dir is None:
