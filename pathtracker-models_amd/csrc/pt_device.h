@@ -310,6 +310,9 @@ template <class S>
 __device__ __forceinline__ f32x16 gemm_pa(const typename Tr<S>::frag (&pa)[Tr<S>::KS],
                                           const typename Tr<S>::frag* __restrict__ g, f32x16 acc,
                                           int lane) {
+  // the fragment loads stay at their use (laundered base): hoisted out of a
+  // row loop as invariants they pinned 8 VGPRs per gate for the whole loop
+  asm volatile("" : "+s"(g));
 #pragma unroll
   for (int s = 0; s < Tr<S>::KS; ++s) acc = Tr<S>::mma(pa[s], g[s * 64 + lane], acc);
   return acc;
