@@ -252,6 +252,21 @@ def main():
                      "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
                      "algorithmic_flop_per_launch": int(flop_launch),
                      "algorithmic_bytes_per_launch": int(byte_launch)})
+        # every kernel kind against its own binding roofline (context for the
+        # dominant one above): conv / wgrad are MFMA-bound, point-wise HBM-bound
+        per_kind = {}
+        for k, (ms, n) in kern.items():
+            fl = algorithmic_flops(k, args.batch, args.frames) * args.steps
+            by = algorithmic_bytes(k, args.batch, args.frames, elt) * args.steps
+            if n == 0 or ms <= 0 or (fl == 0 and by == 0):
+                continue
+            sec = ms * 1e-3
+            if fl / (peak_f * 1e12) >= by / (PEAK_HBM_GBS * 1e9):
+                per_kind[k] = {"bound": "mfma", "achieved_tflops": round(fl / sec / 1e12, 1),
+                               "frac": round(fl / sec / 1e12 / peak_f, 3)}
+            else:
+                per_kind[k] = {"bound": "hbm", "achieved_gbs": round(by / sec / 1e9, 1),
+                               "frac": round(by / sec / 1e9 / PEAK_HBM_GBS, 3)}
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -271,6 +286,7 @@ def main():
                        "frames": args.frames, "channels": C, "kernel": K,
                        "parallelism": f"dp{world}"},
             "roofline": roof,
+            "roofline_per_kernel": per_kind,
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
             "loss": round(float(loss.item()), 5),
         }
