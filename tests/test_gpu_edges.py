@@ -1,0 +1,123 @@
+"""Edge cases and size-independent properties of the HIP cell (InT / hGRU).
+
+* smallest shapes against the CPU oracle (f32, 1e-3): one clip, one frame;
+  an odd batch with two frames; a single-clip 64x64 hGRU (tiles, B=1);
+* the opt-in fused backward (PT_CELL_FUSED=1) against the same oracle;
+* at the headline size (B=256, T=64, bf16) where the oracle is too slow:
+  permutation equivariance (BatchNorm's batch statistics are symmetric in the
+  clips, so permuting the clips permutes the logits; fp64 statistics sums make
+  the result order-independent to rounding) and run-to-run reproducibility.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def _perturbed(cls, t, seed, **kw):
+    torch.manual_seed(seed)
+    m = cls(dimensions=32, timesteps=t, kernel_size=7, **kw)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
+                p.uniform_(0.5, 1.5)
+            elif n.endswith(("mu", "gamma")):
+                p.uniform_(-0.5, 0.5)
+    return m
+
+
+def _close(name, a, b, atol, rtol=0.0):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, np.float64)
+    err = np.abs(a - b).max()
+    assert err <= atol + rtol * np.abs(b).max(), f"{name}: {err:.3e}"
+
+
+def _vs_oracle(m, x, y, hgru=False):
+    from oracle import cells
+    dev = _dev()
+    sd = {k: v.detach().clone().requires_grad_(k != "unit1.w") for k, v in m.named_parameters()}
+    lo, _, _ = cells.recurrent_forward(sd, x, hgru=hgru)
+    cells.bce_logits(lo, y).backward()
+    m = m.to(dev)
+    out, _ = m(x.to(dev))
+    F.binary_cross_entropy_with_logits(out, y.to(dev).reshape(-1, 1)).backward()
+    _close("logits", out, lo, 1e-3)
+    for k, p in m.named_parameters():
+        if p.grad is not None:
+            _close(f"grad {k}", p.grad, sd[k].grad, 1e-6, 1e-3)
+
+
+def _batch(seed, b, t, hw=32):
+    from ptamd import synth
+    clips, labels = synth.make_batch(seed, b, t, h=hw, w=hw)
+    x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float()
+    return x, torch.tensor([ord(v) for v in labels], dtype=torch.float32)
+
+
+@pytest.mark.parametrize("b,t", [(1, 1), (3, 2), (2, 1)])
+def test_int_smallest_shapes(b, t):
+    from models import InT
+    x, y = _batch(20 + b + t, b, t)
+    _vs_oracle(_perturbed(InT.InT, t, seed=b * 10 + t), x, y)
+
+
+def test_hgru_single_clip_tiled():
+    from models import ffhgru_hierarchy as hg
+    x, y = _batch(31, 1, 3, hw=64)
+    _vs_oracle(_perturbed(hg.FFhGRU, 3, seed=5), x, y, hgru=True)
+
+
+@pytest.mark.parametrize("cell", ["int", "hgru"])
+def test_fused_backward_opt_in(cell):
+    from models import InT, ffhgru_hierarchy as hg
+    x, y = _batch(41, 4, 5)
+    m = _perturbed(hg.FFhGRU if cell == "hgru" else InT.InT, 5, seed=9)
+    os.environ["PT_CELL_FUSED"] = "1"
+    try:
+        _vs_oracle(m, x, y, hgru=cell == "hgru")
+    finally:
+        os.environ.pop("PT_CELL_FUSED")
+
+
+def _headline_model(dev):
+    from models import InT
+    torch.manual_seed(1234)
+    m = InT.InT(dimensions=32, timesteps=64, kernel_size=7).to(dev)
+    m.cell_dtype = "bf16"
+    return m
+
+
+def test_headline_size_permutation_and_reproducibility():
+    dev = _dev()
+    import bench
+    x, y = bench.make_data(77, 256, 64, dev)
+    m = _headline_model(dev)
+    perm = torch.randperm(256, generator=torch.Generator().manual_seed(3)).to(dev)
+    out1, _ = m(x)
+    F.binary_cross_entropy_with_logits(out1, y.reshape(-1, 1)).backward()
+    g1 = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    out2, _ = m(x)                                       # same input again
+    F.binary_cross_entropy_with_logits(out2, y.reshape(-1, 1)).backward()
+    _close("rerun logits", out2, out1, 1e-6)
+    for k, p in m.named_parameters():
+        if p.grad is not None:
+            _close(f"rerun grad {k}", p.grad, g1[k], 1e-7, 1e-5)
+    m.zero_grad(set_to_none=True)
+    out3, _ = m(x[perm].contiguous())                    # clips permuted
+    F.binary_cross_entropy_with_logits(out3, y[perm].reshape(-1, 1)).backward()
+    _close("permuted logits", out3, out1[perm], 1e-4)
+    for k, p in m.named_parameters():
+        if p.grad is not None:                           # the mean loss is permutation invariant
+            _close(f"permuted grad {k}", p.grad, g1[k], 1e-6, 2e-3)
