@@ -89,9 +89,9 @@ def algorithmic_bytes(kind, batch, frames, elt):
         "k_conv_fa": frames * 2 * F,
         "k_pw_fb": frames * (XF + 3 * F),
         "k_conv_fb": frames * 2 * F,
-        "k_pw_ba": frames * (XF + 12 * F),
+        "k_pw_ba": frames * (XF + 11 * F),
         "k_conv_ba": (frames - 1) * 5 * F + 3 * F,
-        "k_pw_bb": frames * (XF + 9 * F),
+        "k_pw_bb": frames * (XF + 8 * F),
         "k_conv_bb": frames * 6 * F,
         "k_wgrad": frames * 4 * F,
     }

@@ -773,7 +773,10 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
     if (tail) {
       f32x16 z, xv;
       stem_cl<ACT>(L.xs, yl, h, st, z, xv);
-      f32x16 dx = load_cl(a.dxp + ro, c, h);
+      // this kernel's share of d xbn_tt (a_w^T d_att_pre); k_pw_bb adds the
+      // inhibition path's share to the same stem-gradient sums itself (the
+      // stem gradient is linear in d xbn), so no d xbn tile crosses HBM
+      f32x16 dx = zero16();
       // attention backward of frame tt.  InT at tt = 0 has none (gE_0 =
       // att * E_{-1} = 0); hGRU's att_0 still feeds the gated inhibition.
       if (head || HG) {
@@ -923,8 +926,9 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
   const float m0 = bs[c], rs0 = bs[32 + c];
   const float bi = a.gb[2][c] + a.gb[3][c];
-  float sm[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int slots[6] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B};
+  float sm[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int slots[10] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B,
+                         SM_PW0, SM_PW1, SM_PW2, SM_PB};
   float bs0 = 0.f, bs1 = 0.f;
 
 #pragma unroll 1
@@ -954,7 +958,6 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
     if (a.no_inh) {
       const f32x16 dEn = gemm_pa<S>(pe, a.gt[4], load_cl(a.dEn + ro, c, h), lane);
       store_cl(a.dEn + ro, c, h, dEn);
-      store_cl(a.dxp + ro, c, h, zero16());
     } else {
       f32x16 z, xv;
       stem_cl<ACT>(L.xs, yl, h, st, z, xv);
@@ -1004,7 +1007,13 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
       F pd[Tr<S>::KS];
       cl_to_pa<S>(wscr, dip, lane, pd);
       dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
-      store_cl(a.dxp + ro, c, h, dx);
+      // stem backward of this share (models/InT.py:212-213): dz = dx nl'(z)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const f32x4 xin = L.xs[yl * IMG + cl_x(r, h)];
+        const float dz = dx[r] * Act<ACT>::d(z[r]);
+        sm[6] += dz * xin[0]; sm[7] += dz * xin[1]; sm[8] += dz * xin[2]; sm[9] += dz;
+      }
       dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);
       dIp = gemm_pa<S>(pe, a.gt[4], dIp, lane);
       if constexpr (HG) {
@@ -1022,7 +1031,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   sm[5] = bs0;
   if (!a.no_inh && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64, lane, wave, tid);
   if (a.ablate & 32) return;
-  flush_small<6>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
+  flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5
   if (!a.no_inh) gacc_flush(L.gacc, L.slabl, slab_p, 2, 2, tid);
   gacc_flush(L.gacc + 2 * 1024, L.slabl, slab_p, 4, 2, tid);
