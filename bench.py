@@ -54,7 +54,7 @@ def gate_flops():          # one 1x1 C->C gate conv over one clip frame
     return 2 * C * C * HW * HW
 
 
-def algorithmic_flops(kind, batch, frames):
+def algorithmic_flops(kind, batch, frames, fused_fwd=False):
     """Algorithmic FLOPs of ALL launches of one kernel kind in one step.
 
     Counts the model's contractions only (no recompute): forward conv + gates;
@@ -76,10 +76,15 @@ def algorithmic_flops(kind, batch, frames):
     # fused backward steps = their two halves
     per_clip["k_conv_pw_bb"] = per_clip["k_conv_bb"] + per_clip["k_pw_bb"]
     per_clip["k_conv_pw_ba"] = per_clip["k_conv_ba"] + per_clip["k_pw_ba"]
+    # fused forward steps (k_pw_conv_fa / k_pw_conv_fb; k_pw_fa then only closes frame T-1)
+    per_clip["k_pw_conv_fa"] = per_clip["k_pw_fa"] + per_clip["k_conv_fa"]
+    per_clip["k_pw_conv_fb"] = per_clip["k_pw_fb"] + per_clip["k_conv_fb"]
+    if fused_fwd:
+        per_clip["k_pw_fa"] = 0
     return per_clip.get(kind, 0) * batch
 
 
-def algorithmic_bytes(kind, batch, frames, elt):
+def algorithmic_bytes(kind, batch, frames, elt, fused_fwd=False):
     """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
     (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
     XF = one clip-frame of the f32 input (3x32x32)."""
@@ -99,6 +104,13 @@ def algorithmic_bytes(kind, batch, frames, elt):
     # that the point-wise half re-reads from L2 in the same workgroup
     per_clip["k_conv_pw_bb"] = per_clip["k_conv_bb"] + per_clip["k_pw_bb"] - frames * F
     per_clip["k_conv_pw_ba"] = per_clip["k_conv_ba"] + per_clip["k_pw_ba"] - (frames - 1) * F
+    # fused forward steps: the conv takes its input from the prologue's LDS tile
+    # (gE_t / I_t still go to HBM for the backward); frame 0 has nothing to
+    # close, which the standalone k_pw_fa(T) (reads I, E, eg, ce; writes E) does
+    per_clip["k_pw_conv_fa"] = frames * (XF + 8 * F) - 5 * F
+    per_clip["k_pw_conv_fb"] = frames * (XF + 4 * F)
+    if fused_fwd:
+        per_clip["k_pw_fa"] = 5 * F
     return per_clip.get(kind, 0) * batch
 
 
@@ -237,8 +249,9 @@ def main():
         dom_ms, dom_n = kern[dom]
         avg_ms = dom_ms / max(dom_n, 1)
         elt = 2 if args.dtype == "bf16" else 4
-        flop_launch = algorithmic_flops(dom, args.batch, args.frames) * args.steps / max(dom_n, 1)
-        byte_launch = algorithmic_bytes(dom, args.batch, args.frames, elt) * args.steps / max(dom_n, 1)
+        ffw = kern["k_pw_conv_fa"][1] > 0
+        flop_launch = algorithmic_flops(dom, args.batch, args.frames, ffw) * args.steps / max(dom_n, 1)
+        byte_launch = algorithmic_bytes(dom, args.batch, args.frames, elt, ffw) * args.steps / max(dom_n, 1)
         peak_f = PEAK_TFLOPS[args.dtype]
         # the binding roofline: the larger of the two ideal times
         if flop_launch / (peak_f * 1e12) >= byte_launch / (PEAK_HBM_GBS * 1e9):
@@ -256,8 +269,8 @@ def main():
         # dominant one above): conv / wgrad are MFMA-bound, point-wise HBM-bound
         per_kind = {}
         for k, (ms, n) in kern.items():
-            fl = algorithmic_flops(k, args.batch, args.frames) * args.steps
-            by = algorithmic_bytes(k, args.batch, args.frames, elt) * args.steps
+            fl = algorithmic_flops(k, args.batch, args.frames, ffw) * args.steps
+            by = algorithmic_bytes(k, args.batch, args.frames, elt, ffw) * args.steps
             if n == 0 or ms <= 0 or (fl == 0 and by == 0):
                 continue
             sec = ms * 1e-3

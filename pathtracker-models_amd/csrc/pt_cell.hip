@@ -245,7 +245,7 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out
 //   EPI_ADD     out = conv + add0 (+ add1), f32
 //   EPI_NONE    fill only (frame 0's dci: needed by k_wgrad, conv^T dead)
 // =========================================================================
-enum { FILL_COPY = 0, FILL_BNBWD = 1 };
+enum { FILL_COPY = 0, FILL_BNBWD = 1, FILL_PRO = 2 };   // FILL_PRO: a prologue writes the tile
 enum { EPI_FWD = 0, EPI_ADD = 1, EPI_NONE = 2 };
 
 template <class S>
@@ -282,8 +282,13 @@ struct StoreRow {
   }
 };
 
-template <class S, int FILL, int EPI>
-__device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b) {
+struct NoPro {
+  template <class T> __device__ __forceinline__ void operator()(T*) const {}
+};
+
+template <class S, int FILL, int EPI, class Pro = NoPro>
+__device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b,
+                                          const Pro& pro = Pro()) {
   S* tile = (S*)smem;
   float* red = (float*)(smem + tile_bytes<S>());
   float* tbl = red + 128;       // FILL_BNBWD: per-channel A, Bc, Cc
@@ -310,6 +315,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
   }
   if constexpr (EPI != EPI_NONE) tile_zero<S>(tile, tid);
   __syncthreads();
+  if constexpr (FILL == FILL_PRO) pro(tile);     // writes the interior (conv_run's barriers follow)
 
   const bool tiled = a.ntx * a.nty > 1;
   auto bnbwd16 = [&](const u32x4& dv, const u32x4& rv, int ch0) {
@@ -331,7 +337,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
         tile_halo<S>(tile, b, a.ntx, a.nty, pass, tid,
                      [&](size_t e, int) { return *(const u32x4*)(a.src + e); });
       tile_fill<S>(tile, a.src + cb, pass, tid);
-    } else {
+    } else if constexpr (FILL == FILL_BNBWD) {
       if (EPI != EPI_NONE && tiled)
         tile_halo<S>(tile, b, a.ntx, a.nty, pass, tid, [&](size_t e, int ch0) {
           return bnbwd16(*(const u32x4*)(a.dc + e), *(const u32x4*)(a.raw + e), ch0);
@@ -566,40 +572,36 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int 
 //           eg = sig(e_w I_{t-1} + e_u gE) (:171, uses the OLD inhibition;
 //           no_inh: e_w E_{t-1}, :168)
 // -------------------------------------------------------------------------
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
-  static_assert(PWF_RPP == 1, "forward point-wise kernels: one row per wave");
-  using F = typename Tr<S>::frag;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.ablate & 512) return;
-  const PLds L = pcarve<PWF_RPP>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
-  const int t = a.t, T = a.T, B = a.B;
-  const int y0 = part * PW_NW;
-  const int yl = wave, y = y0 + yl;
-  float* wscr = L.scr + wave * SCR_FLOATS;
-  const size_t fs = fr_off(1, B), ro = clip_off(b) + (size_t)y * IMG * C;
-
-  // this wave's row tiles first: their latency overlaps the staging below
-  Pk<S> Iv = zero_pk<S>(), Eo = zero_pk<S>(), egv = zero_pk<S>(), cev = zero_pk<S>();
+template <class S> struct FaIn { Pk<S> Iv, Eo, egv, cev; };
+template <class S>
+__device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, size_t ro, int c, int h) {
+  const size_t fs = fr_off(1, a.B);
+  const int t = a.t;
+  FaIn<S> w;
+  w.Iv = zero_pk<S>(); w.Eo = zero_pk<S>(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
   if (t > 0) {
-    Iv = load_pk(a.I + (t - 1) * fs + ro, c, h);
-    if (t >= 2) Eo = load_pk(a.E + (t - 2) * fs + ro, c, h);
-    egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
-    cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
+    w.Iv = load_pk(a.I + (t - 1) * fs + ro, c, h);
+    if (t >= 2) w.Eo = load_pk(a.E + (t - 2) * fs + ro, c, h);
+    w.egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
+    w.cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
   }
-  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
-  if (t > 0)
-    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
-                    blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
-  __syncthreads();
-  if (a.ablate & 4) return;
+  return w;
+}
 
+// One image row of forward point-wise A (x of the row staged in xs, BN1 stats
+// of frame t-1 in stat[64..127]).  tile (fused kernel): gE_t also goes into
+// the conv's LDS tile.
+template <class S, int ACT, int HG>
+__device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
+                                       int yl, float* wscr, int b, int y, size_t ro,
+                                       const FaIn<S>& in, int lane, S* tile) {
+  using F = typename Tr<S>::frag;
+  const int c = lane & 31, h = lane >> 5;
+  const int t = a.t, T = a.T;
+  const size_t fs = fr_off(1, a.B);
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float kap = a.kappa[c], gam = a.gamma[c], bw1 = a.bnw1[c], bb1 = a.bnb1[c];
-  const float m1 = L.stat[64 + c], rs1 = L.stat[96 + c];
+  const float m1 = stat[64 + c], rs1 = stat[96 + c];
   const float ba = a.gb[0][c] + a.gb[1][c], be = a.gb[4][c] + a.gb[5][c];
 
   // close frame t-1 (:172-175)
@@ -608,16 +610,16 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
     const float A1 = bw1 * rs1, B1 = bb1 - bw1 * rs1 * m1;     // BN1 affine folded
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float cn = A1 * (float)cev[r] + B1;
-      const float eh = Act<ACT>::f(cn * (kap * (float)Iv[r] + gam));
-      const float e = (float)egv[r];
-      Ep[r] = (1.f - e) * (float)Eo[r] + e * eh;
+      const float cn = A1 * (float)in.cev[r] + B1;
+      const float eh = Act<ACT>::f(cn * (kap * (float)in.Iv[r] + gam));
+      const float e = (float)in.egv[r];
+      Ep[r] = (1.f - e) * (float)in.Eo[r] + e * eh;
     }
     store_cl(a.E + (t - 1) * fs + ro, c, h, Ep);
   }
   if (t == T) return;
   f32x16 z, xv;
-  stem_cl<ACT>(L.xs, yl, h, st, z, xv);
+  stem_cl<ACT>(xs, yl, h, st, z, xv);
   F pax[Tr<S>::KS], pae[Tr<S>::KS];
   cl_to_pa<S>(wscr, xv, lane, pax);
   cl_to_pa<S>(wscr, Ep, lane, pae);
@@ -628,6 +630,10 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) { att[r] = sigm(acc[r] + ba); gEv[r] = att[r] * Ep[r]; }
   store_cl(a.gE + t * fs + ro, c, h, gEv);
+  if (tile) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[tile_off<S>(y + PADMAX, cl_x(r, h) + PADMAX, c)] = (S)gEv[r];
+  }
   if (a.gates) {
     const TileLoc tl = tile_loc(b, a.ntx, a.nty);
     const int W = a.ntx * IMG;
@@ -644,7 +650,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   } else if (a.no_inh) {
     cl_to_pa<S>(wscr, Ep, lane, pai);
   } else {
-    cl_to_pa<S>(wscr, Iv, lane, pai);
+    cl_to_pa<S>(wscr, in.Iv, lane, pai);
   }
   acc = zero16();
   acc = gemm_pa<S>(pai, a.gf[4], acc, lane);
@@ -655,14 +661,9 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   store_cl(a.eg + t * fs + ro, c, h, egn);
 }
 
-// -------------------------------------------------------------------------
-// Forward point-wise B (frame t): BN0 -> Ihat = nl(x - nl(c_i (alpha I + mu)))
-//   (:162), ig = sig(i_w x + i_u I) (:165), I_t = (1-ig) I + ig Ihat (:166)
-//   [no_inh: I_t = gE (:168)]
-// -------------------------------------------------------------------------
 template <class S, int ACT, int HG>
-__global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
-  using F = typename Tr<S>::frag;
+__global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
+  static_assert(PWF_RPP == 1, "forward point-wise kernels: one row per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (a.ablate & 512) return;
   const PLds L = pcarve<PWF_RPP>(smem);
@@ -672,7 +673,88 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   const int t = a.t, T = a.T, B = a.B;
   const int y0 = part * PW_NW;
   const int yl = wave, y = y0 + yl;
-  float* wscr = L.scr + wave * SCR_FLOATS;
+  const size_t ro = clip_off(b) + (size_t)y * IMG * C;
+  // this wave's row tiles first: their latency overlaps the staging below
+  const FaIn<S> in = fa_load(a, ro, c, h);
+  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
+  if (t > 0)
+    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
+                    blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
+  __syncthreads();
+  if (a.ablate & 4) return;
+  fa_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, b, y, ro, in, lane, nullptr);
+}
+
+// -------------------------------------------------------------------------
+// Forward point-wise B (frame t): BN0 -> Ihat = nl(x - nl(c_i (alpha I + mu)))
+//   (:162), ig = sig(i_w x + i_u I) (:165), I_t = (1-ig) I + ig Ihat (:166)
+//   [no_inh: I_t = gE (:168)]
+// -------------------------------------------------------------------------
+template <class S> struct FbIn { Pk<S> civ, Iv, gi; };
+template <class S, int HG>
+__device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, size_t ro, int c, int h) {
+  const size_t fs = fr_off(1, a.B);
+  const int t = a.t;
+  FbIn<S> w;
+  w.civ = load_pk(a.ci + t * fs + ro, c, h);
+  w.Iv = t > 0 ? load_pk(a.I + (t - 1) * fs + ro, c, h) : zero_pk<S>();
+  if constexpr (HG) w.gi = load_pk(a.at + t * fs + ro, c, h);   // gated inhibition att_t
+  else w.gi = w.Iv;                                             // InT: I_{t-1}
+  return w;
+}
+
+// One image row of forward point-wise B (BN0 stats of frame t in stat[0..63]);
+// tile (fused kernel): I_t also goes into the conv's LDS tile.
+template <class S, int ACT, int HG>
+__device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
+                                       int yl, float* wscr, int y, size_t ro, const FbIn<S>& in,
+                                       int lane, S* tile) {
+  using F = typename Tr<S>::frag;
+  const int c = lane & 31, h = lane >> 5;
+  const size_t fs = fr_off(1, a.B);
+  const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
+  const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
+  const float m0 = stat[c], rs0 = stat[32 + c];
+  const float A0 = bw0 * rs0, B0 = bb0 - bw0 * rs0 * m0;     // BN0 affine folded
+  const float bi = a.gb[2][c] + a.gb[3][c];
+
+  f32x16 z, xv, ih;
+  stem_cl<ACT>(xs, yl, h, st, z, xv);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float cn = A0 * (float)in.civ[r] + B0;
+    ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * (float)in.gi[r] + mu)));
+  }
+  F pax[Tr<S>::KS], pai[Tr<S>::KS];
+  cl_to_pa<S>(wscr, xv, lane, pax);
+  cl_to_pa<S>(wscr, in.gi, lane, pai);
+  f32x16 acc = zero16();
+  acc = gemm_pa<S>(pax, a.gf[2], acc, lane);
+  acc = gemm_pa<S>(pai, a.gf[3], acc, lane);
+  f32x16 In;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float ig = sigm(acc[r] + bi);
+    In[r] = (1.f - ig) * (float)in.Iv[r] + ig * ih[r];
+  }
+  store_cl(a.I + a.t * fs + ro, c, h, In);
+  if (tile) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[tile_off<S>(y + PADMAX, cl_x(r, h) + PADMAX, c)] = (S)In[r];
+  }
+}
+
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.ablate & 512) return;
+  const PLds L = pcarve<PWF_RPP>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
+  const int t = a.t, T = a.T, B = a.B;
+  const int y0 = part * PW_NW;
+  const int yl = wave, y = y0 + yl;
   const size_t fs = fr_off(1, B), ro = clip_off(b) + (size_t)y * IMG * C;
 
   if (a.no_inh) {      // I_t = gE_t (:168)
@@ -685,43 +767,98 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
     }
     return;
   }
-  const Pk<S> civ = load_pk(a.ci + t * fs + ro, c, h);
-  const Pk<S> Iv = t > 0 ? load_pk(a.I + (t - 1) * fs + ro, c, h) : zero_pk<S>();
-  Pk<S> gi;                    // gated inhibition: I_{t-1} (InT) / att_t (hGRU)
-  if constexpr (HG) gi = load_pk(a.at + t * fs + ro, c, h);
-  else gi = Iv;
+  const FbIn<S> in = fb_load<S, HG>(a, ro, c, h);
   stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, B, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
+  fb_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, y, ro, in, lane, nullptr);
+}
 
-  const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
-  const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
-  const float m0 = L.stat[c], rs0 = L.stat[32 + c];
-  const float A0 = bw0 * rs0, B0 = bb0 - bw0 * rs0 * m0;     // BN0 affine folded
-  const float bi = a.gb[2][c] + a.gb[3][c];
-
-  f32x16 z, xv, ih;
-  stem_cl<ACT>(L.xs, yl, h, st, z, xv);
+// -------------------------------------------------------------------------
+// Fused forward frame steps (bf16, one 32x32 tile per clip): the point-wise
+// work whose output is a conv's input runs as the conv kernel's prologue in
+// the same workgroup and writes the conv's LDS tile directly (and its HBM copy
+// for the backward), so the conv input is never re-read and a launch per step
+// is saved.  No grid-wide dependency lies between them: the prologue needs the
+// previous conv's BatchNorm statistics, which the launch boundary provides.
+//   k_pw_conv_fa(t): point-wise A (close frame t-1, att, gE_t, eg_t) + conv(gE_t, w_inh)
+//   k_pw_conv_fb(t): point-wise B (BN0, I_t) + conv(I_t, w_exc)
+// The prologue's rows (8 per wave) load their tiles in groups so the loads
+// overlap; its scratch (x rows, transposes, stats) sits above the conv's LDS.
+// Frames made of several tiles keep the separate kernels (the conv halo would
+// need the neighbours' prologue output).
+// -------------------------------------------------------------------------
+template <class S>
+constexpr int fwdx_lds_bytes() {
+  return conv_lds_bytes<S>() + NPIX * 16 /*x rows*/ + NWAVE * SCR_FLOATS * 4 + 128 * 4;
+}
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(NT, 1) void k_pw_conv_fa(ConvArgs<S> ca, CellArgs<S> a) {
+  if constexpr (sizeof(S) == 2) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    f32x4* xs = (f32x4*)(smem + conv_lds_bytes<S>());
+    float* scr = (float*)(xs + NPIX);
+    float* stat = scr + NWAVE * SCR_FLOATS;
+    auto pro = [&](S* tile) {
+      const int t = a.t;
+      // rolling prefetch: G rows' tiles in flight, the first ones under the staging
+      constexpr int G = 4;
+      FaIn<S> in[G];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float cn = A0 * (float)civ[r] + B0;
-    ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * (float)gi[r] + mu)));
-  }
-  F pax[Tr<S>::KS], pai[Tr<S>::KS];
-  cl_to_pa<S>(wscr, xv, lane, pax);
-  cl_to_pa<S>(wscr, gi, lane, pai);
-  f32x16 acc = zero16();
-  acc = gemm_pa<S>(pax, a.gf[2], acc, lane);
-  acc = gemm_pa<S>(pai, a.gf[3], acc, lane);
-  f32x16 In;
+      for (int i = 0; i < G; ++i)
+        in[i] = fa_load(a, clip_off(b) + (size_t)(wave * RPW + i) * IMG * C, c, h);
+      stage_x(a.x, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
+      if (t > 0)
+        bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, a.B, a.eps, stat + 64,
+                        b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
+      __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float ig = sigm(acc[r] + bi);
-    In[r] = (1.f - ig) * (float)Iv[r] + ig * ih[r];
+      for (int j = 0; j < RPW; ++j) {
+        const int y = wave * RPW + j;
+        const FaIn<S> cur = in[j % G];
+        if (j + G < RPW)
+          in[j % G] = fa_load(a, clip_off(b) + (size_t)(y + G) * IMG * C, c, h);
+        fa_row<S, ACT, HG>(a, stat, xs, y, scr + wave * SCR_FLOATS, b, y,
+                           clip_off(b) + (size_t)y * IMG * C, cur, lane, tile);
+      }
+    };
+    conv_body<S, FILL_PRO, EPI_FWD>(ca, smem, b, pro);
   }
-  store_cl(a.I + t * fs + ro, c, h, In);
+}
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(NT, 1) void k_pw_conv_fb(ConvArgs<S> ca, CellArgs<S> a) {
+  if constexpr (sizeof(S) == 2) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    f32x4* xs = (f32x4*)(smem + conv_lds_bytes<S>());
+    float* scr = (float*)(xs + NPIX);
+    float* stat = scr + NWAVE * SCR_FLOATS;
+    auto pro = [&](S* tile) {
+      const int t = a.t;
+      FbIn<S> in[RPW];                // all 8 rows' tiles in flight under the staging
+#pragma unroll
+      for (int i = 0; i < RPW; ++i)
+        in[i] = fb_load<S, HG>(a, clip_off(b) + (size_t)(wave * RPW + i) * IMG * C, c, h);
+      stage_x(a.x, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
+      bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, a.B, a.eps, stat,
+                      b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        const int y = wave * RPW + i;
+        fb_row<S, ACT, HG>(a, stat, xs, y, scr + wave * SCR_FLOATS, y,
+                           clip_off(b) + (size_t)y * IMG * C, in[i], lane, tile);
+      }
+    };
+    conv_body<S, FILL_PRO, EPI_FWD>(ca, smem, b, pro);
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -1616,6 +1753,7 @@ void timed(int kind, hipStream_t st, F&& launch) {
 }
 
 bool fused_enabled();
+bool fused_fwd_enabled();
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
@@ -1782,6 +1920,11 @@ int set_lds_attrs() {
   SETLDS((k_conv_pw_ba<S, A, H, EPI_NONE>), fused_lds_bytes<S>());
   SETLDS_FUSED(0, 0) SETLDS_FUSED(0, 1) SETLDS_FUSED(1, 0) SETLDS_FUSED(1, 1)
 #undef SETLDS_FUSED
+#define SETLDS_FWDX(A, H)                                                          \
+  SETLDS((k_pw_conv_fa<S, A, H>), fwdx_lds_bytes<S>());                            \
+  SETLDS((k_pw_conv_fb<S, A, H>), fwdx_lds_bytes<S>());
+  SETLDS_FWDX(0, 0) SETLDS_FWDX(0, 1) SETLDS_FWDX(1, 0) SETLDS_FWDX(1, 1)
+#undef SETLDS_FWDX
   done = true;
   return 0;
 }
@@ -1820,7 +1963,16 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
   ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
   ca.wf = a.wf_inh;
   cb.wf = a.wf_exc;
-  for (int t = 0; t <= p.T; ++t) {
+  const bool fx = sizeof(S) == 2 && p.ntx * p.nty == 1 && !d->no_inh && fused_fwd_enabled();
+  const size_t lfu = fwdx_lds_bytes<S>();
+  for (int t = 0; t < p.T && fx; ++t) {
+    a.t = t;
+    ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96;
+    timed(PT_K_FWD_A, st, [&] { FUSED_LAUNCH(k_pw_conv_fa, , ca); });
+    cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * NBNC * 96;
+    timed(PT_K_FWD_B, st, [&] { FUSED_LAUNCH(k_pw_conv_fb, , cb); });
+  }
+  for (int t = fx ? p.T : 0; t <= p.T; ++t) {
     a.t = t;
     timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });
     if (t == p.T) break;
@@ -1951,6 +2103,17 @@ bool fused_enabled() {
   const char* f = getenv("PT_CELL_FUSED");
   return f && atoi(f) != 0;
 }
+// PT_CELL_FUSED_FWD=1 selects the fused forward frame steps (k_pw_conv_fa /
+// k_pw_conv_fb; bf16 single-tile frames with an inhibitory conv only).  Off by
+// default for the same reason as the fused backward: measured slower (B=256
+// T=64 bf16: 77 us vs 36 + 34 us for pw_fa + conv_fa, 62 vs 23 + 34 us for
+// pw_fb + conv_fb; 10.3k vs 10.8k clips/s), the prologue's 8 rows per wave at
+// one wave per SIMD expose the latency the 8-workgroup point-wise launches hide,
+// and saving the conv's re-read of its input (3 us of HBM time) cannot pay that.
+bool fused_fwd_enabled() {
+  const char* f = getenv("PT_CELL_FUSED_FWD");
+  return f && atoi(f) != 0;
+}
 int ablate_env() {
   const char* ab = getenv("PT_CELL_ABLATE");
   return ab ? atoi(ab) : 0;
@@ -1982,7 +2145,8 @@ int pt_cell_forward(const pt_cell_desc* d, const float* x, const pt_cell_params*
   if (!use_graph()) return body(st);
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
-  k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env());
+  k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env())
+      .add((int)fused_fwd_enabled());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 
