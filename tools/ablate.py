@@ -41,8 +41,8 @@ def main():
             lib.pt_cell_timing_enable(0)
             if r == 0:
                 continue
-            for kind, name in enumerate(kinds):
-                ms, n = _lib.timing_read(kind)
+            for name in kinds:
+                ms, n = _lib.timing_read(_lib.KIND_NAMES.index(name))
                 if n:
                     res[mk][name].append(1e3 * ms / n)
     os.environ.pop("PT_CELL_ABLATE")
