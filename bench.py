@@ -84,11 +84,11 @@ def algorithmic_flops(kind, batch, frames, fused_fwd=False):
     return per_clip.get(kind, 0) * batch
 
 
-def algorithmic_bytes(kind, batch, frames, elt, fused_fwd=False):
+def algorithmic_bytes(kind, batch, frames, elt, fused_fwd=False, xb=4):
     """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
     (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
-    XF = one clip-frame of the f32 input (3x32x32)."""
-    F, XF = C * HW * HW * elt, 3 * HW * HW * 4
+    XF = one clip-frame of the input (3x32x32; xb = 4 B f32, 1 B raw u8 clips)."""
+    F, XF = C * HW * HW * elt, 3 * HW * HW * xb
     per_clip = {
         "k_pw_fa": frames * (XF + 7 * F),
         "k_conv_fa": frames * 2 * F,
@@ -127,10 +127,13 @@ def pmc_traffic(kernel, batch, frames, dtype):
     return None
 
 
-def make_data(seed, batch, frames, device):
+def make_data(seed, batch, frames, device, u8=False):
+    """Synthetic clips: the f32 model input [B,3,T,32,32], or (u8) the raw
+    clip bytes [B,T,32,32,3] the cell converts while staging each frame."""
     from ptamd import synth
     clips, labels = synth.make_batch(seed, batch, frames)
-    x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3).astype(np.float32) / 255.0)
+    x = (torch.from_numpy(clips) if u8 else
+         torch.from_numpy(clips.transpose(0, 4, 1, 2, 3).astype(np.float32) / 255.0))
     y = torch.tensor([ord(b) for b in labels], dtype=torch.float32)
     return x.to(device), y.to(device)
 
@@ -178,6 +181,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--input", default="f32", choices=["u8", "f32"],
+                    help="cell input: raw u8 clips (converted in-kernel) or the f32 tensor")
     args = ap.parse_args()
 
     from ptamd import _lib
@@ -199,7 +204,7 @@ def main():
     bucket = GradBucket(model.parameters(), dev)
     opt = torch.optim.Adam(model.parameters(), lr=3e-4)
     crit = torch.nn.BCEWithLogitsLoss()
-    x, y = make_data(1000 + rank, args.batch, args.frames, dev)
+    x, y = make_data(1000 + rank, args.batch, args.frames, dev, u8=args.input == "u8")
 
     def step():
         out, _ = model(x)
@@ -250,8 +255,9 @@ def main():
         avg_ms = dom_ms / max(dom_n, 1)
         elt = 2 if args.dtype == "bf16" else 4
         ffw = kern["k_pw_conv_fa"][1] > 0
+        xb = 1 if args.input == "u8" else 4
         flop_launch = algorithmic_flops(dom, args.batch, args.frames, ffw) * args.steps / max(dom_n, 1)
-        byte_launch = algorithmic_bytes(dom, args.batch, args.frames, elt, ffw) * args.steps / max(dom_n, 1)
+        byte_launch = algorithmic_bytes(dom, args.batch, args.frames, elt, ffw, xb) * args.steps / max(dom_n, 1)
         peak_f = PEAK_TFLOPS[args.dtype]
         # the binding roofline: the larger of the two ideal times
         if flop_launch / (peak_f * 1e12) >= byte_launch / (PEAK_HBM_GBS * 1e9):
@@ -270,7 +276,7 @@ def main():
         per_kind = {}
         for k, (ms, n) in kern.items():
             fl = algorithmic_flops(k, args.batch, args.frames, ffw) * args.steps
-            by = algorithmic_bytes(k, args.batch, args.frames, elt, ffw) * args.steps
+            by = algorithmic_bytes(k, args.batch, args.frames, elt, ffw, xb) * args.steps
             if n == 0 or ms <= 0 or (fl == 0 and by == 0):
                 continue
             sec = ms * 1e-3
@@ -294,9 +300,9 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic",
             "config": {"workload": f"InT 32x32x{args.frames}f fwd+BPTT+Adam, "
-                                   f"{args.batch} clips/GPU, {args.dtype} cell",
+                                   f"{args.batch} clips/GPU, {args.dtype} cell, {args.input} input",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
-                       "frames": args.frames, "channels": C, "kernel": K,
+                       "frames": args.frames, "channels": C, "kernel": K, "input": args.input,
                        "parallelism": f"dp{world}"},
             "roofline": roof,
             "roofline_per_kernel": per_kind,

@@ -37,8 +37,16 @@ enum { PT_ACT_SOFTPLUS = 0, PT_ACT_TANH = 1 };      /* the model's `nl` (models/
 enum { PT_CELL_INT = 0, PT_CELL_HGRU = 1 };         /* rCell / hConvGRUCell */
 enum { PT_DTYPE_F32 = 0, PT_DTYPE_BF16 = 1 };       /* storage + MFMA operand type */
 
-/* Problem description.  Layout of the input x: [B][3][T][H][W] fp32 (what
- * engine.prepare_data produces, utils/engine.py:220-255). */
+/* Input layouts (pt_cell_desc.x_format):
+ *  PT_X_F32_NCTHW  x = f32 [B][3][T][H][W], the model input as
+ *                  engine.prepare_data produces it (utils/engine.py:220-255);
+ *  PT_X_U8_NTHWC   x = u8 [B][T][H][W][3], the raw clip bytes as the TFRecords
+ *                  hold them (utils/TFRDataset.py:6-28); the kernels convert
+ *                  each byte u to (float)(u / 255.0 in double), bit-identical to
+ *                  prepare_data's plain branch, so the f32 tensor is never built. */
+enum { PT_X_F32_NCTHW = 0, PT_X_U8_NTHWC = 1 };
+
+/* Problem description. */
 typedef struct pt_cell_desc {
     int32_t batch;      /* B  clips on this device                              */
     int32_t channels;   /* C  = `dimensions` (utils/engine.py:75); must be 32  */
@@ -51,6 +59,7 @@ typedef struct pt_cell_desc {
     int32_t cell;       /* PT_CELL_*                                            */
     int32_t dtype;      /* PT_DTYPE_*                                           */
     float   eps;        /* BatchNorm eps (1e-3, models/InT.py:102)              */
+    int32_t x_format;   /* PT_X_*                                               */
 } pt_cell_desc;
 
 /* Recurrent-cell parameters, fp32, PyTorch layouts.  Gate order everywhere:
@@ -92,7 +101,7 @@ size_t pt_cell_workspace_bytes(const pt_cell_desc* d);
  *           the readout, models/InT.py:236)
  *   gates   [B,T,C,H,W] fp32 out or NULL: attention maps (testmode, :230-233)
  */
-int pt_cell_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* p,
+int pt_cell_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* p,
                     void* saved, void* workspace, float* e_last, float* gates,
                     pt_stream_t stream);
 
@@ -104,7 +113,7 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq,
 /* BPTT backward (replaces autograd through the frame loop).
  *   d_e_last  [B,C,H,W] fp32: dLoss/d e_last from the readout.
  * Writes every parameter gradient (overwrite, not accumulate). */
-int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* p,
+int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* p,
                      const void* saved, void* workspace, const float* d_e_last,
                      const pt_cell_grads* g, pt_stream_t stream);
 

@@ -60,7 +60,8 @@ struct CellArgs {
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
                   // atomics, 16 skip the 1x1 weight-gradient LDS reductions,
                   // 32 skip slab flush
-  const float* x;                       // [B][3][T][32][32]
+  const void* x;                        // f32 [B][3][T][H][W] or u8 [B][T][H][W][3] (xu8)
+  int xu8;
   const float *wpre, *bpre;             // [32][3], [32]
   const float *alpha, *mu, *gamma, *kappa;
   const float *bnw0, *bnb0, *bnw1, *bnb1;
@@ -98,12 +99,31 @@ __device__ __forceinline__ TileLoc tile_loc(int v, int ntx, int nty) {
   return {b, ty, q - ty * ntx};
 }
 
-// Stage rows [y0, y0+nrows) of tile v of x[:, 0:3, t] (x is [clips][3][T][H][W])
-// as float4 per pixel.
-__device__ void stage_x(const float* __restrict__ x, f32x4* xs, int v, int t, int T, int y0,
-                        int nrows, int tid, int nthreads, int ntx, int nty) {
+// Stage rows [y0, y0+nrows) of tile v of x[:, 0:3, t] as float4 per pixel.
+// x is either the model input f32 [clips][3][T][H][W] or (xu8) the raw clip
+// bytes u8 [clips][T][H][W][3] as the TFRecords hold them, converted here
+// exactly as engine.prepare_data does (utils/engine.py:220-255: the float64
+// quotient u / 255 rounded to f32), so the f32 tensor never has to exist.
+__device__ void stage_x(const void* __restrict__ xv, int xu8, f32x4* xs, int v, int t, int T,
+                        int y0, int nrows, int tid, int nthreads, int ntx, int nty) {
   const TileLoc L = tile_loc(v, ntx, nty);
   const int W = ntx * IMG;
+  if (xu8) {
+    const uint8_t* x = (const uint8_t*)xv +
+                       (((size_t)L.b * T + t) * ((size_t)nty * IMG) + L.ty * IMG + y0) * W * 3 +
+                       (size_t)L.tx * IMG * 3;
+    for (int p = tid; p < nrows * IMG; p += nthreads) {
+      const uint8_t* q = x + ((size_t)(p >> 5) * W + (p & 31)) * 3;
+      f32x4 v4;
+      v4[0] = (float)((double)q[0] / 255.0);
+      v4[1] = (float)((double)q[1] / 255.0);
+      v4[2] = (float)((double)q[2] / 255.0);
+      v4[3] = 0.f;
+      xs[p] = v4;
+    }
+    return;
+  }
+  const float* x = (const float*)xv;
   const size_t plane = (size_t)nty * IMG * W;
   const size_t o = (size_t)(L.ty * IMG + y0) * W + L.tx * IMG;
   const float* x0 = x + ((size_t)(L.b * 3 + 0) * T + t) * plane + o;
@@ -676,7 +696,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   const size_t ro = clip_off(b) + (size_t)y * IMG * C;
   // this wave's row tiles first: their latency overlaps the staging below
   const FaIn<S> in = fa_load(a, ro, c, h);
-  if (t < T) stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
+  if (t < T) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   if (t > 0)
     bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
@@ -768,7 +788,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
     return;
   }
   const FbIn<S> in = fb_load<S, HG>(a, ro, c, h);
-  stage_x(a.x, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
+  stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, B, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
@@ -812,7 +832,7 @@ __global__ __launch_bounds__(NT, 1) void k_pw_conv_fa(ConvArgs<S> ca, CellArgs<S
 #pragma unroll
       for (int i = 0; i < G; ++i)
         in[i] = fa_load(a, clip_off(b) + (size_t)(wave * RPW + i) * IMG * C, c, h);
-      stage_x(a.x, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
+      stage_x(a.x, a.xu8, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
       if (t > 0)
         bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, a.B, a.eps, stat + 64,
                         b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
@@ -846,7 +866,7 @@ __global__ __launch_bounds__(NT, 1) void k_pw_conv_fb(ConvArgs<S> ca, CellArgs<S
 #pragma unroll
       for (int i = 0; i < RPW; ++i)
         in[i] = fb_load<S, HG>(a, clip_off(b) + (size_t)(wave * RPW + i) * IMG * C, c, h);
-      stage_x(a.x, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
+      stage_x(a.x, a.xu8, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
       bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, a.B, a.eps, stat,
                       b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
       __syncthreads();
@@ -887,7 +907,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
   slab_prefetch(slab_p, L.slabl, 0, 2, wave, lane);        // a_w, a_u
-  if (tail) stage_x(a.x, L.xs, b, tt, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
+  if (tail) stage_x(a.x, a.xu8, L.xs, b, tt, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   gacc_zero(L.gacc, 2, tid);
   __syncthreads();
 
@@ -1054,7 +1074,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   BbRow<S> pre;
   if constexpr (RPP == 1) pre = load_row(clip_off(b) + (size_t)(y0 + wave) * IMG * C);
   slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);        // i_w, i_u, e_w, e_u
-  stage_x(a.x, L.xs, b, t, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
+  stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   gacc_zero(L.gacc, 4, tid);
   __syncthreads();
 
@@ -1783,6 +1803,8 @@ int check(const pt_cell_desc* d) {
   if (d->dtype != PT_DTYPE_F32 && d->dtype != PT_DTYPE_BF16) return fail(PT_ERR_ARG, "bad dtype%s%ld");
   if (d->cell != PT_CELL_INT && d->cell != PT_CELL_HGRU) return fail(PT_ERR_ARG, "bad cell%s%ld");
   if (d->cell == PT_CELL_HGRU && d->no_inh) return fail(PT_ERR_ARG, "no_inh is an InT option%s%ld");
+  if (d->x_format != PT_X_F32_NCTHW && d->x_format != PT_X_U8_NTHWC)
+    return fail(PT_ERR_ARG, "bad x_format%s (got %ld)", "", d->x_format);
   return 0;
 }
 
@@ -1819,7 +1841,7 @@ Plan plan(const pt_cell_desc* d) {
 }
 
 template <class S>
-void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float* x,
+void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void* x,
                const pt_cell_params* pr, char* saved, char* ws) {
   using F = typename Tr<S>::frag;
   memset(&a, 0, sizeof(a));
@@ -1827,6 +1849,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const float
   a.ntx = p.ntx; a.nty = p.nty;
   a.hgru = d->cell == PT_CELL_HGRU;
   a.x = x;
+  a.xu8 = d->x_format == PT_X_U8_NTHWC;
   {
     const char* ab = getenv("PT_CELL_ABLATE");     // timing experiments only
     a.ablate = ab ? atoi(ab) : 0;
@@ -1939,7 +1962,7 @@ ConvArgs<S> conv_args(const CellArgs<S>& a) {
 }
 
 template <class S>
-int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr, void* saved,
+int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, void* saved,
                 void* ws, float* e_last, float* gates, hipStream_t st) {
   const Plan p = plan(d);
   if (int rc = set_lds_attrs<S>()) return rc;
@@ -1994,7 +2017,7 @@ int run_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
 }
 
 template <class S>
-int run_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* pr,
+int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
                  const void* saved, void* ws, const float* d_e_last, const pt_cell_grads* g,
                  hipStream_t st) {
   const Plan p = plan(d);
@@ -2132,7 +2155,7 @@ size_t pt_cell_workspace_bytes(const pt_cell_desc* d) {
   return plan(d).ws;
 }
 
-int pt_cell_forward(const pt_cell_desc* d, const float* x, const pt_cell_params* p, void* saved,
+int pt_cell_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* p, void* saved,
                     void* ws, float* e_last, float* gates, pt_stream_t stream) {
   if (int rc = check(d)) return rc;
   if (!x || !p || !saved || !ws) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
@@ -2166,7 +2189,7 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, p
   return 0;
 }
 
-int pt_cell_backward(const pt_cell_desc* d, const float* x, const pt_cell_params* p,
+int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* p,
                      const void* saved, void* ws, const float* d_e_last, const pt_cell_grads* g,
                      pt_stream_t stream) {
   if (int rc = check(d)) return rc;

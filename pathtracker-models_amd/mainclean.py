@@ -54,13 +54,15 @@ def validate(args, val_loader, model, criterion, device, results_folder, len_val
              logiters=None):
     """mainclean.py:54-98: mean loss / accuracy / precision / recall / f1 over
     the validation batches (only the first logiters + 2 when logiters is set)."""
+    keep_u8 = getattr(model, 'accepts_u8', False) and not args.f32_input
     batch_timev, lossesv, top1v = AverageMeter(), AverageMeter(), AverageMeter()
     precisionv, recallv, f1scorev = AverageMeter(), AverageMeter(), AverageMeter()
     end = time.time()
     with torch.no_grad():
         for i, (imgs, target) in enumerate(val_loader):
             imgs, target = engine.prepare_data(imgs=imgs, target=target, args=args, device=device,
-                                               disentangle_channels=disentangle_channels)
+                                               disentangle_channels=disentangle_channels,
+                                               keep_u8=keep_u8)
             output, jv_penalty = engine.model_step(model, imgs, model_name=args.model)
             loss = criterion(output, target.float().reshape(-1, 1))
             prec1, preci, rec, f1s = acc_scores(target, output.data)
@@ -159,6 +161,9 @@ def main(argv=None):
             dist.broadcast(p.data, 0)
     print("Loading finished" if world == 1 else f"data-parallel over {world} ranks")
     bucket = GradBucket(model.parameters(), device)
+    # HIP-cell models take the raw u8 clips: the /255 conversion and the
+    # [B,T,H,W,3] -> [B,3,T,H,W] transpose happen while the kernels stage x
+    keep_u8 = getattr(model, 'accepts_u8', False) and not args.f32_input
 
     if main_rank:
         param_names_shapes = {k: v.shape for k, v in model.named_parameters()}
@@ -187,7 +192,8 @@ def main(argv=None):
                 break
             data_time.update(time.perf_counter() - end)
             imgs, target = engine.prepare_data(imgs=imgs, target=target, args=args, device=device,
-                                               disentangle_channels=disentangle_channels)
+                                               disentangle_channels=disentangle_channels,
+                                               keep_u8=keep_u8)
             output, jv_penalty = engine.model_step(model, imgs, model_name=args.model)
             loss = criterion(output, target.float().reshape(-1, 1))
             losses.update(loss.data.item(), 1)

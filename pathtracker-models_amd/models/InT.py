@@ -21,7 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn import init
 
-from ptamd.cell import PARAM_KEYS, CellConfig, run_cell
+from ptamd.cell import PARAM_KEYS, CellConfig, run_cell, target_channel
 
 _DEFAULT_DTYPE = os.environ.get("PT_CELL_DTYPE", "f32")
 
@@ -142,10 +142,14 @@ class InT(nn.Module):
 
     def readout(self, e_last, x):
         """models/InT.py:236-241"""
-        out = torch.cat([self.readout_conv(e_last), x[:, 2, 0][:, None]], 1)
+        out = torch.cat([self.readout_conv(e_last), target_channel(x)[:, None]], 1)
         out = self.target_conv(out)
         out = F.avg_pool2d(out, kernel_size=out.size()[2:])
         return self.readout_dense(out.reshape(x.shape[0], -1))
+
+    # forward also takes the raw u8 clips [B,T,H,W,3] (engine.prepare_data
+    # keep_u8): the kernels convert them exactly as prepare_data would
+    accepts_u8 = True
 
     def forward(self, x, testmode=False):
         e_last, e_seq, gates = run_cell(x, self.cell_params(), self.cell_config(),

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "libptcell.so")
 PT_ACT_SOFTPLUS, PT_ACT_TANH = 0, 1
 PT_CELL_INT, PT_CELL_HGRU = 0, 1
 PT_DTYPE_F32, PT_DTYPE_BF16 = 0, 1
+PT_X_F32_NCTHW, PT_X_U8_NTHWC = 0, 1
 
 # Exported symbols declared in include/pt_cell.h (tests check all are present).
 EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
@@ -37,7 +38,7 @@ class Desc(ctypes.Structure):
                 ("width", ctypes.c_int32), ("ksize", ctypes.c_int32),
                 ("act", ctypes.c_int32), ("no_inh", ctypes.c_int32),
                 ("cell", ctypes.c_int32), ("dtype", ctypes.c_int32),
-                ("eps", ctypes.c_float)]
+                ("eps", ctypes.c_float), ("x_format", ctypes.c_int32)]
 
 
 class Params(ctypes.Structure):

@@ -45,13 +45,38 @@ _UNUSED_NO_INH = {"unit1.w_inh", "unit1.alpha", "unit1.mu", "unit1.i_w_gate.weig
                   "unit1.bn.0.weight", "unit1.bn.0.bias"}
 
 
+def clip_dims(x: torch.Tensor):
+    """(B, T, H, W) of a model input: f32 [B,3,T,H,W] or raw u8 clips [B,T,H,W,3]."""
+    if x.dtype == torch.uint8:
+        b, t, h, w, ch = x.shape
+    else:
+        b, ch, t, h, w = x.shape
+    if ch != 3:
+        raise ValueError(f"expected 3 input channels, got shape {tuple(x.shape)}")
+    return b, t, h, w
+
+
+def unit_values(x_u8: torch.Tensor) -> torch.Tensor:
+    """u8 -> f32 exactly as engine.prepare_data (float64 u / 255 rounded to f32)."""
+    return (x_u8.to(torch.float64) / 255.).to(torch.float32)
+
+
+def target_channel(x: torch.Tensor) -> torch.Tensor:
+    """x[:, 2, 0] of the f32 model input (the readout's target marker,
+    models/InT.py:236) from either input layout."""
+    if x.dtype == torch.uint8:
+        return unit_values(x[:, 0, :, :, 2])
+    return x[:, 2, 0]
+
+
 def _desc(cfg: CellConfig, x: torch.Tensor, channels: int) -> _lib.Desc:
-    b, _, t, h, w = x.shape
+    b, t, h, w = clip_dims(x)
     return _lib.Desc(batch=b, channels=channels, frames=t, height=h, width=w, ksize=cfg.ksize,
                      act=_lib.PT_ACT_TANH if cfg.act == "tanh" else _lib.PT_ACT_SOFTPLUS,
                      no_inh=int(cfg.no_inh),
                      cell=_lib.PT_CELL_HGRU if cfg.cell == "hgru" else _lib.PT_CELL_INT,
-                     dtype=DTYPES[cfg.dtype], eps=cfg.eps)
+                     dtype=DTYPES[cfg.dtype], eps=cfg.eps,
+                     x_format=_lib.PT_X_U8_NTHWC if x.dtype == torch.uint8 else _lib.PT_X_F32_NCTHW)
 
 
 def _ptr(t):
@@ -81,7 +106,10 @@ def _require_device(x):
 
 
 class RecurrentCellFn(torch.autograd.Function):
-    """(x [B,3,T,H,W], params...) -> (E_T [B,C,H,W], E_seq [B,T,C,H,W], att [B,T,C,H,W]).
+    """(x, params...) -> (E_T [B,C,H,W], E_seq [B,T,C,H,W], att [B,T,C,H,W]).
+
+    x is the f32 model input [B,3,T,H,W] or the raw u8 clips [B,T,H,W,3]
+    (converted inside the kernels, bit-identical to engine.prepare_data).
 
     E_seq / att are only filled when ``want_seq`` (testmode); otherwise they
     are empty tensors.  Only E_T is differentiable.
@@ -91,7 +119,7 @@ class RecurrentCellFn(torch.autograd.Function):
     def forward(ctx, x, cfg: CellConfig, want_seq: bool, *params):
         _require_device(x)
         lib = _lib.load()
-        x = x.contiguous().float()
+        x = x.contiguous() if x.dtype == torch.uint8 else x.contiguous().float()
         params = [p.contiguous().float() if p is not None else None for p in params]
         c = params[0].shape[0]
         d = _desc(cfg, x, c)
@@ -101,7 +129,7 @@ class RecurrentCellFn(torch.autograd.Function):
             _lib.check(1)
         ws = torch.empty(lib.pt_cell_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                          device=x.device)
-        b, _, t, h, w = x.shape
+        b, t, h, w = clip_dims(x)
         e_last = torch.empty((b, c, h, w), dtype=torch.float32, device=x.device)
         gates = torch.empty((b, t, c, h, w) if want_seq else (0,), dtype=torch.float32,
                             device=x.device)
@@ -129,7 +157,8 @@ class RecurrentCellFn(torch.autograd.Function):
         c = params[0].shape[0]
         d = _desc(ctx.cfg, x, c)
         if d_e_last is None:
-            d_e_last = torch.zeros((x.shape[0], c, x.shape[3], x.shape[4]), device=x.device)
+            b, _, h, w = clip_dims(x)
+            d_e_last = torch.zeros((b, c, h, w), device=x.device)
         d_e_last = d_e_last.contiguous().float()
         ws = torch.empty(lib.pt_cell_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                          device=x.device)

@@ -104,19 +104,25 @@ def _u8_to_unit(device):
     return lut
 
 
-def prepare_data(imgs, target, args, device, disentangle_channels, use_augmentations=False):
+def prepare_data(imgs, target, args, device, disentangle_channels, use_augmentations=False,
+                 keep_u8=False):
     """uint8 [B,T,H,W,3] clips + byte labels -> fp32 [B,3,T,H,W] in [0,1] + float labels.
 
     Reference: utils/engine.py:220-255.  ``imgs`` may be a numpy array or a
     torch tensor (host or device); ``target`` an array of 1-byte strings, of
-    uint8, or a tensor of codes.
+    uint8, or a tensor of codes.  ``keep_u8`` (models with ``accepts_u8``, i.e.
+    the HIP-cell InT / FFhGRU): the plain branch returns the device u8 clips
+    unchanged and the cell's kernels do the identical conversion while staging
+    each frame (include/pt_cell.h PT_X_U8_NTHWC).
     """
     if use_augmentations:
         raise NotImplementedError("use_augmentations: the reference's transform is undefined there")
     device = torch.device(device)
     u8 = imgs if isinstance(imgs, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(imgs))
     u8 = u8.to(device)       # synchronous: the loader reuses its pinned host buffers
-    if not disentangle_channels:
+    if keep_u8 and not disentangle_channels and not getattr(args, 'pretrained', False):
+        x = u8.contiguous()
+    elif not disentangle_channels:
         x = _u8_to_unit(device)[u8.long()].permute(0, 4, 1, 2, 3).contiguous()
     else:
         # mask = round(sum_c u_c/255) in float64, as numpy does (:227-232)

@@ -58,3 +58,5 @@ parser.add_argument('--data-root', type=str, default=None)
 parser.add_argument('--synthetic', type=int, default=0)
 parser.add_argument('--results-root', type=str, default=None)
 parser.add_argument('--max-iters', type=int, default=0)
+parser.add_argument('--f32-input', default=False, action='store_true',
+                    help='hand the HIP-cell models the f32 [B,3,T,H,W] tensor instead of the raw u8 clips')

@@ -3,6 +3,9 @@
 * smallest shapes against the CPU oracle (f32, 1e-3): one clip, one frame;
   an odd batch with two frames; a single-clip 64x64 hGRU (tiles, B=1);
 * the opt-in fused backward (PT_CELL_FUSED=1) against the same oracle;
+* raw u8 clips [B,T,H,W,3] as the cell input (PT_X_U8_NTHWC) against the
+  f32 tensor engine.prepare_data builds from them: same values, so logits and
+  gradients agree to fp64-atomic summation order (InT f32 / bf16, tiled hGRU);
 * the opt-in fused bf16 forward frame steps (k_pw_conv_fa / k_pw_conv_fb,
   PT_CELL_FUSED_FWD=1) against the separate launches: same rounding
   points, so logits and gradients agree to fp64-atomic summation order;
@@ -118,6 +121,36 @@ def test_fused_forward_matches_separate(cell):
     _close("logits", o1, o0, 1e-5)
     for k in g0:
         _close(f"grad {k}", g1[k], g0[k], 1e-7, 1e-4)
+
+
+@pytest.mark.parametrize("cell,dtype,hw", [("int", "f32", 32), ("int", "bf16", 32),
+                                           ("hgru", "bf16", 64)])
+def test_u8_input_matches_f32_input(cell, dtype, hw):
+    import types
+    from models import InT, ffhgru_hierarchy as hg
+    from ptamd import synth
+    from utils import engine
+    dev = _dev()
+    clips, labels = synth.make_batch(47, 4, 5, h=hw, w=hw)
+    args = types.SimpleNamespace(pretrained=False)
+    x, y = engine.prepare_data(clips, labels, args, dev, False)
+    xu, _ = engine.prepare_data(clips, labels, args, dev, False, keep_u8=True)
+    assert xu.dtype == torch.uint8
+    m = _perturbed(hg.FFhGRU if cell == "hgru" else InT.InT, 5, seed=13).to(dev)
+    m.cell_dtype = dtype
+    res = []
+    for inp in (x, xu):
+        m.zero_grad(set_to_none=True)
+        out, _ = m(inp)
+        F.binary_cross_entropy_with_logits(out, y.reshape(-1, 1)).backward()
+        res.append((out.detach().clone(), {k: p.grad.detach().clone()
+                                           for k, p in m.named_parameters() if p.grad is not None}))
+    (o0, g0), (o1, g1) = res
+    assert torch.isfinite(o1).all()
+    _close("logits", o1, o0, 1e-6)
+    assert g0.keys() == g1.keys()
+    for k in g0:
+        _close(f"grad {k}", g1[k], g0[k], 1e-7, 1e-5)
 
 
 def _headline_model(dev):

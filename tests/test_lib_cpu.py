@@ -69,6 +69,38 @@ def test_size_queries_and_validation():
         big.height, big.width = h, w
         assert lib.pt_cell_saved_bytes(ctypes.byref(big)) == 0
         assert b"multiple of 32" in lib.pt_last_error()
+    # input layouts: f32 [B,3,T,H,W] (0) or raw u8 clips [B,T,H,W,3] (1); same sizes
+    d.x_format = _lib.PT_X_U8_NTHWC
+    assert lib.pt_cell_saved_bytes(ctypes.byref(d)) == saved
+    d.x_format = 2
+    assert lib.pt_cell_saved_bytes(ctypes.byref(d)) == 0
+    assert b"x_format" in lib.pt_last_error()
+
+
+def test_u8_input_helpers_match_prepare_data():
+    """The u8 input path's conversion and readout target are bit-identical to
+    engine.prepare_data's f32 tensor (utils/engine.py:220-255)."""
+    import types
+    import numpy as np
+    import torch
+    from ptamd import cell, synth
+    from utils import engine
+    clips, labels = synth.make_batch(5, 3, 4, h=32, w=32)
+    args = types.SimpleNamespace(pretrained=False)
+    x, y = engine.prepare_data(clips, labels, args, "cpu", False)
+    xu, yu = engine.prepare_data(clips, labels, args, "cpu", False, keep_u8=True)
+    assert xu.dtype == torch.uint8 and tuple(xu.shape) == clips.shape
+    assert torch.equal(yu, y)
+    assert torch.equal(cell.unit_values(xu).permute(0, 4, 1, 2, 3), x)
+    assert torch.equal(cell.target_channel(xu), x[:, 2, 0])
+    assert cell.clip_dims(xu) == cell.clip_dims(x) == (3, 4, 32, 32)
+    # every byte value, against numpy's float64 quotient
+    allv = torch.arange(256, dtype=torch.uint8)
+    ref = (np.arange(256, dtype=np.float64) / 255.).astype(np.float32)
+    assert np.array_equal(cell.unit_values(allv).numpy(), ref)
+    # disentangle / pretrained keep the f32 path
+    xd, _ = engine.prepare_data(clips, labels, args, "cpu", True, keep_u8=True)
+    assert xd.dtype == torch.float32
 
 
 @pytest.mark.parametrize("tag", ["int_c32", "int_noinh", "int_lesion"])
