@@ -9,9 +9,13 @@ Synthetic seeded PathTracker clips (ptamd.synth), resident in HBM before the
 timed region; random init (no checkpoints offline).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
-N>1 is launched by torch.distributed.run (one rank per GPU, RCCL); rank 0
-prints ONE JSON line.  value = clips/s of the whole job (all ranks) =
+N>1: one rank per GPU over RCCL.  Under torch.distributed.run the ranks come
+from the environment (WORLD_SIZE must equal N); run directly, bench.py starts
+torch.distributed.run itself as a child process before touching the GPU.  Rank
+0 prints ONE JSON line.  value = clips/s of the whole job (all ranks) =
 N * B * K / max-over-ranks(time of K steps).  Scaling is weak (B fixed per GPU).
+allreduce_ms_per_step: device time of the gradient all-reduce (exposed: the
+cell's weight gradients are all final only when the BPTT sweep reaches t=0).
 
 roofline: the dominant kernel (largest summed device time over K further,
 instrumented steps, measured with HIP events the library records around its
@@ -20,13 +24,18 @@ HBM bandwidth — using the algorithmic FLOPs / bytes per launch of DESIGN.md §
 traffic = PMC-measured HBM bytes per launch from profiles/ (or null).
 cpu_baseline: the CPU oracle
 (oracle/cells.py, plain PyTorch fp32, the reference's own op graph) timed on
-this host for a bounded sample (rank 0, N=1 only).
+this host for a bounded sample (rank 0, N=1 only): B=4 clips of the workload's
+64 frames, and (cpu_baseline_cfg1) BASELINE configs[0]'s B=4 x 32 frames.
+f32_cell: the same step with the f32 cell (the reference's arithmetic and the
+parity path) at the same size, a precision-matched figure beside the bf16 value.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -54,7 +63,7 @@ def gate_flops():          # one 1x1 C->C gate conv over one clip frame
     return 2 * C * C * HW * HW
 
 
-def algorithmic_flops(kind, batch, frames, fused_fwd=False):
+def algorithmic_flops(kind, batch, frames):
     """Algorithmic FLOPs of ALL launches of one kernel kind in one step.
 
     Counts the model's contractions only (no recompute): forward conv + gates;
@@ -73,21 +82,15 @@ def algorithmic_flops(kind, batch, frames, fused_fwd=False):
         "k_pw_bb": frames * 8 * gf,                 # i_*, e_* dgrad + wgrad
         "k_wgrad": frames * 2 * cf,                 # dW_inh + dW_exc
     }
-    # fused backward steps = their two halves
-    per_clip["k_conv_pw_bb"] = per_clip["k_conv_bb"] + per_clip["k_pw_bb"]
-    per_clip["k_conv_pw_ba"] = per_clip["k_conv_ba"] + per_clip["k_pw_ba"]
-    # fused forward steps (k_pw_conv_fa / k_pw_conv_fb; k_pw_fa then only closes frame T-1)
-    per_clip["k_pw_conv_fa"] = per_clip["k_pw_fa"] + per_clip["k_conv_fa"]
-    per_clip["k_pw_conv_fb"] = per_clip["k_pw_fb"] + per_clip["k_conv_fb"]
-    if fused_fwd:
-        per_clip["k_pw_fa"] = 0
     return per_clip.get(kind, 0) * batch
 
 
-def algorithmic_bytes(kind, batch, frames, elt, fused_fwd=False, xb=4):
+def algorithmic_bytes(kind, batch, frames, elt, xb=4):
     """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
     (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
-    XF = one clip-frame of the input (3x32x32; xb = 4 B f32, 1 B raw u8 clips)."""
+    XF = one clip-frame of the input (3x32x32; xb = 4 B f32, 1 B raw u8 clips).
+    Implementation overhead (the per-workgroup gradient partials, BatchNorm
+    sums) is not algorithmic and is not counted."""
     F, XF = C * HW * HW * elt, 3 * HW * HW * xb
     per_clip = {
         "k_pw_fa": frames * (XF + 7 * F),
@@ -100,31 +103,62 @@ def algorithmic_bytes(kind, batch, frames, elt, fused_fwd=False, xb=4):
         "k_conv_bb": frames * 6 * F,
         "k_wgrad": frames * 4 * F,
     }
-    # fused backward steps: both halves minus the hand-off tensor (dI_t / dgE_t)
-    # that the point-wise half re-reads from L2 in the same workgroup
-    per_clip["k_conv_pw_bb"] = per_clip["k_conv_bb"] + per_clip["k_pw_bb"] - frames * F
-    per_clip["k_conv_pw_ba"] = per_clip["k_conv_ba"] + per_clip["k_pw_ba"] - (frames - 1) * F
-    # fused forward steps: the conv takes its input from the prologue's LDS tile
-    # (gE_t / I_t still go to HBM for the backward); frame 0 has nothing to
-    # close, which the standalone k_pw_fa(T) (reads I, E, eg, ce; writes E) does
-    per_clip["k_pw_conv_fa"] = frames * (XF + 8 * F) - 5 * F
-    per_clip["k_pw_conv_fb"] = frames * (XF + 4 * F)
-    if fused_fwd:
-        per_clip["k_pw_fa"] = 5 * F
     return per_clip.get(kind, 0) * batch
 
 
-def pmc_traffic(kernel, batch, frames, dtype):
+def pmc_traffic(kernel, batch, frames, dtype, lib_version):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from
-    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same workload), or None."""
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same workload), or None.
+    Only a summary stamped with the loaded library's version (which carries the
+    hash of the kernel sources, ptamd/build.py) counts: counters of other
+    kernels say nothing about these."""
     import glob
     tag = f"B={batch} T={frames} {dtype}"
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
         d = json.load(open(f))
-        if d.get("note") == tag and kernel in d.get("kernels", {}):
+        if (d.get("note") == tag and d.get("lib_version") == lib_version
+                and kernel in d.get("kernels", {})):
             return d["kernels"][kernel]["traffic_bytes"]
     return None
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(argv, gpus, script=None):
+    """--gpus N > 1 outside a torch.distributed.run launch: start N ranks of
+    `script` (default: this file) on this node as a child process (before this
+    process touches the GPU) and return its exit code; None when this process
+    is already a rank or N = 1."""
+    if gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(script or __file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(world, rank):
+    """--dry-run: the launcher and rendezvous path with gloo on CPU, no GPU:
+    every rank checks the world size and joins one all-reduce."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        assert int(t.item()) == world
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def make_data(seed, batch, frames, device, u8=False):
@@ -171,6 +205,24 @@ def cpu_baseline(seconds, frames=64, batch=4):
                       f"{n} steps in {el:.1f}s"}
 
 
+def kernel_roofline(kind, ms, n, batch, frames, steps, dtype, xb):
+    """One kernel kind against whichever roofline binds it (the larger ideal
+    time: algorithmic FLOP / dense MFMA peak vs algorithmic bytes / HBM peak)."""
+    elt = 2 if dtype == "bf16" else 4
+    fl = algorithmic_flops(kind, batch, frames) * steps / max(n, 1)
+    by = algorithmic_bytes(kind, batch, frames, elt, xb) * steps / max(n, 1)
+    avg = ms / max(n, 1) * 1e-3
+    peak_f = PEAK_TFLOPS[dtype]
+    if fl / (peak_f * 1e12) >= by / (PEAK_HBM_GBS * 1e9):
+        r = {"bound": "mfma", "achieved": round(fl / avg / 1e12, 2), "peak": peak_f,
+             "unit": "TFLOP/s"}
+    else:
+        r = {"bound": "hbm", "achieved": round(by / avg / 1e9, 1), "peak": PEAK_HBM_GBS,
+             "unit": "GB/s"}
+    r["frac"] = round(r["achieved"] / r["peak"], 4)
+    return r, int(fl), int(by), avg * 1e3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,44 +231,69 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="clips per GPU")
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-f32", action="store_true", help="skip the f32-cell figure")
+    ap.add_argument("--f32-steps", type=int, default=3)
     ap.add_argument("--input", default="f32", choices=["u8", "f32"],
                     help="cell input: raw u8 clips (converted in-kernel) or the f32 tensor")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous check on CPU (gloo), no GPU work")
     args = ap.parse_args()
 
-    from ptamd import _lib
+    rc = launch_ranks(sys.argv[1:], args.gpus)
+    if rc is not None:
+        sys.exit(rc)
     from ptamd.dist import GradBucket, env_rank
+    rank, local_rank, world = env_rank()
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dry_run:
+        dry_run(world, rank)
+        return
+
+    from ptamd import _lib
     from models import InT as int_mod
 
-    rank, local_rank, world = env_rank()
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        assert dist.get_world_size() == args.gpus and dist.get_backend() == "nccl"
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    torch.manual_seed(1234)
-    model = int_mod.InT(dimensions=C, timesteps=args.frames, kernel_size=K).to(dev)
-    model.cell_dtype = args.dtype
-    if world > 1:                       # identical init on every rank
-        for p in model.parameters():
-            dist.broadcast(p.data, 0)
-    bucket = GradBucket(model.parameters(), dev)
-    opt = torch.optim.Adam(model.parameters(), lr=3e-4)
+    def build(dtype):
+        torch.manual_seed(1234)
+        model = int_mod.InT(dimensions=C, timesteps=args.frames, kernel_size=K).to(dev)
+        model.cell_dtype = dtype
+        if world > 1:                       # identical init on every rank
+            for p in model.parameters():
+                dist.broadcast(p.data, 0)
+        return (model, GradBucket(model.parameters(), dev),
+                torch.optim.Adam(model.parameters(), lr=3e-4))
+
+    model, bucket, opt = build(args.dtype)
     crit = torch.nn.BCEWithLogitsLoss()
     x, y = make_data(1000 + rank, args.batch, args.frames, dev, u8=args.input == "u8")
+    ar_ev = []                               # (start, end) events around the all-reduce
 
-    def step():
+    def step(model, bucket, opt, time_ar=False):
         out, _ = model(x)
         loss = crit(out, y.reshape(-1, 1))
         loss.backward()
-        bucket.allreduce_mean()
+        if time_ar and world > 1:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            bucket.allreduce_mean()
+            e1.record()
+            ar_ev.append((e0, e1))
+        else:
+            bucket.allreduce_mean()
         opt.step()
         opt.zero_grad(set_to_none=True)
         return loss
 
     for _ in range(args.warmup):
-        step()
+        step(model, bucket, opt)
     torch.cuda.synchronize()
     lib = _lib.load()
     # timed region: no instrumentation (the per-launch HIP events of the
@@ -226,66 +303,67 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = step(model, bucket, opt)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # kernel-timing pass (same steps, HIP events around every library launch)
+    # kernel-timing pass (same steps, HIP events around every library launch
+    # on its launch stream, and around the all-reduce)
     lib.pt_cell_timing_reset()
     lib.pt_cell_timing_enable((1 << _lib.NKINDS) - 1)
     for _ in range(args.steps):
-        step()
+        step(model, bucket, opt, time_ar=True)
     torch.cuda.synchronize()
     lib.pt_cell_timing_enable(0)
-    kern = {}
-    for kind, name in enumerate(_lib.KIND_NAMES):
-        ms, n = _lib.timing_read(kind)
-        kern[name] = (ms, n)
+    kern = {name: _lib.timing_read(kind) for kind, name in enumerate(_lib.KIND_NAMES)}
     lib.pt_cell_timing_reset()
+    ar_ms = sum(a.elapsed_time(b) for a, b in ar_ev) / args.steps if ar_ev else 0.0
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el, ar_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el, ar_ms = float(t[0]), float(t[1])
+    version = lib.pt_version().decode()
+    f32 = None
+    if world == 1 and args.dtype == "bf16" and not args.no_f32:
+        del model, bucket, opt
+        torch.cuda.empty_cache()
+        m32, b32, o32 = build("f32")
+        step(m32, b32, o32)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.f32_steps):
+            step(m32, b32, o32)
+        torch.cuda.synchronize()
+        e32 = time.perf_counter() - t1
+        f32 = {"value": round(args.batch * args.f32_steps / e32, 2), "unit": "clips/s",
+               "ms_per_step": round(e32 / args.f32_steps * 1e3, 3), "steps": args.f32_steps,
+               "dtype": "f32",
+               "note": "same step with the f32 cell (exact-f32 MFMA, f32 saved states): the "
+                       "reference's arithmetic and the oracle-pinned parity path"}
+        del m32, b32, o32
 
     if rank == 0:
+        xb = 1 if args.input == "u8" else 4
         value = world * args.batch * args.steps / el
         dom = max(kern, key=lambda k: kern[k][0])
         dom_ms, dom_n = kern[dom]
-        avg_ms = dom_ms / max(dom_n, 1)
-        elt = 2 if args.dtype == "bf16" else 4
-        ffw = kern["k_pw_conv_fa"][1] > 0
-        xb = 1 if args.input == "u8" else 4
-        flop_launch = algorithmic_flops(dom, args.batch, args.frames, ffw) * args.steps / max(dom_n, 1)
-        byte_launch = algorithmic_bytes(dom, args.batch, args.frames, elt, ffw, xb) * args.steps / max(dom_n, 1)
-        peak_f = PEAK_TFLOPS[args.dtype]
-        # the binding roofline: the larger of the two ideal times
-        if flop_launch / (peak_f * 1e12) >= byte_launch / (PEAK_HBM_GBS * 1e9):
-            roof = {"bound": "mfma", "achieved": round(flop_launch / (avg_ms * 1e-3) / 1e12, 2),
-                    "peak": peak_f, "unit": "TFLOP/s"}
-        else:
-            roof = {"bound": "hbm", "achieved": round(byte_launch / (avg_ms * 1e-3) / 1e9, 1),
-                    "peak": PEAK_HBM_GBS, "unit": "GB/s"}
-        roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-        roof.update({"traffic": pmc_traffic(dom, args.batch, args.frames, args.dtype),
+        roof, fl, by, avg_ms = kernel_roofline(dom, dom_ms, dom_n, args.batch, args.frames,
+                                               args.steps, args.dtype, xb)
+        roof.update({"traffic": pmc_traffic(dom, args.batch, args.frames, args.dtype, version),
                      "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
-                     "algorithmic_flop_per_launch": int(flop_launch),
-                     "algorithmic_bytes_per_launch": int(byte_launch)})
+                     "algorithmic_flop_per_launch": fl, "algorithmic_bytes_per_launch": by})
         # every kernel kind against its own binding roofline (context for the
         # dominant one above): conv / wgrad are MFMA-bound, point-wise HBM-bound
         per_kind = {}
         for k, (ms, n) in kern.items():
-            fl = algorithmic_flops(k, args.batch, args.frames, ffw) * args.steps
-            by = algorithmic_bytes(k, args.batch, args.frames, elt, ffw, xb) * args.steps
-            if n == 0 or ms <= 0 or (fl == 0 and by == 0):
+            if n == 0 or ms <= 0 or (algorithmic_flops(k, 1, args.frames) == 0 and
+                                     algorithmic_bytes(k, 1, args.frames, 2) == 0):
                 continue
-            sec = ms * 1e-3
-            if fl / (peak_f * 1e12) >= by / (PEAK_HBM_GBS * 1e9):
-                per_kind[k] = {"bound": "mfma", "achieved_tflops": round(fl / sec / 1e12, 1),
-                               "frac": round(fl / sec / 1e12 / peak_f, 3)}
-            else:
-                per_kind[k] = {"bound": "hbm", "achieved_gbs": round(by / sec / 1e9, 1),
-                               "frac": round(by / sec / 1e9 / PEAK_HBM_GBS, 3)}
+            r, _, _, a = kernel_roofline(k, ms, n, args.batch, args.frames, args.steps,
+                                         args.dtype, xb)
+            per_kind[k] = {"bound": r["bound"], "achieved": r["achieved"], "unit": r["unit"],
+                           "frac": r["frac"], "avg_launch_us": round(a * 1e3, 2)}
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -307,12 +385,17 @@ def main():
             "roofline": roof,
             "roofline_per_kernel": per_kind,
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
+            "allreduce_ms_per_step": round(ar_ms, 4),
+            "lib_version": version,
             "loss": round(float(loss.item()), 5),
         }
+        if f32 is not None:
+            line["f32_cell"] = f32
         if not np.isfinite(line["loss"]):
             print("bench.py: WARNING non-finite training loss", file=sys.stderr, flush=True)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, frames=args.frames)
+            line["cpu_baseline_cfg1"] = cpu_baseline(args.cpu_seconds, frames=32)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -126,11 +126,7 @@ int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params*
 enum { PT_K_PW_FA = 0, PT_K_CONV_FA = 1, PT_K_PW_FB = 2, PT_K_CONV_FB = 3,
        PT_K_PW_BA = 4, PT_K_CONV_BA = 5, PT_K_PW_BB = 6, PT_K_CONV_BB = 7,
        PT_K_WGRAD = 8, PT_K_PREP = 9, PT_K_REDUCE = 10,
-       PT_K_BWD_C = 11,   /* fused k_conv_pw_bb: conv^T(w_exc) + point-wise B backward */
-       PT_K_BWD_D = 12,   /* fused k_conv_pw_ba: conv^T(w_inh) + point-wise A backward */
-       PT_K_FWD_A = 13,   /* fused k_pw_conv_fa: point-wise A forward + conv(w_inh) */
-       PT_K_FWD_B = 14,   /* fused k_pw_conv_fb: point-wise B forward + conv(w_exc) */
-       PT_K_NKINDS = 15 };
+       PT_K_NKINDS = 11 };
 int pt_cell_timing_enable(uint32_t kind_mask);      /* bit k enables kind k; 0 disables */
 int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches);
 int pt_cell_timing_reset(void);

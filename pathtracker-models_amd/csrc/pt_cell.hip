@@ -265,7 +265,7 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out
 //   EPI_ADD     out = conv + add0 (+ add1), f32
 //   EPI_NONE    fill only (frame 0's dci: needed by k_wgrad, conv^T dead)
 // =========================================================================
-enum { FILL_COPY = 0, FILL_BNBWD = 1, FILL_PRO = 2 };   // FILL_PRO: a prologue writes the tile
+enum { FILL_COPY = 0, FILL_BNBWD = 1 };
 enum { EPI_FWD = 0, EPI_ADD = 1, EPI_NONE = 2 };
 
 template <class S>
@@ -302,13 +302,8 @@ struct StoreRow {
   }
 };
 
-struct NoPro {
-  template <class T> __device__ __forceinline__ void operator()(T*) const {}
-};
-
-template <class S, int FILL, int EPI, class Pro = NoPro>
-__device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b,
-                                          const Pro& pro = Pro()) {
+template <class S, int FILL, int EPI>
+__device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b) {
   S* tile = (S*)smem;
   float* red = (float*)(smem + tile_bytes<S>());
   float* tbl = red + 128;       // FILL_BNBWD: per-channel A, Bc, Cc
@@ -335,7 +330,6 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
   }
   if constexpr (EPI != EPI_NONE) tile_zero<S>(tile, tid);
   __syncthreads();
-  if constexpr (FILL == FILL_PRO) pro(tile);     // writes the interior (conv_run's barriers follow)
 
   const bool tiled = a.ntx * a.nty > 1;
   auto bnbwd16 = [&](const u32x4& dv, const u32x4& rv, int ch0) {
@@ -432,10 +426,21 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
     }
   }
 }
-template <class S, int FILL, int EPI>
-__global__ __launch_bounds__(NT, 1) void k_conv(ConvArgs<S> a) {
+// Distinct kernel names per role (rocprof summaries tell them apart).
+template <class S>
+__global__ __launch_bounds__(NT, 1) void k_conv_fwd(ConvArgs<S> a) {     // conv + BN partials
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL, EPI>(a, smem, blockIdx.x);
+  conv_body<S, FILL_COPY, EPI_FWD>(a, smem, blockIdx.x);
+}
+template <class S>
+__global__ __launch_bounds__(NT, 1) void k_conv_bwd(ConvArgs<S> a) {     // BN bwd + conv^T + adds
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_body<S, FILL_BNBWD, EPI_ADD>(a, smem, blockIdx.x);
+}
+template <class S>
+__global__ __launch_bounds__(NT, 1) void k_bnbwd_fill(ConvArgs<S> a) {   // frame 0: BN bwd only
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_body<S, FILL_BNBWD, EPI_NONE>(a, smem, blockIdx.x);
 }
 
 // =========================================================================
@@ -609,12 +614,11 @@ __device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, size_t ro, int 
 }
 
 // One image row of forward point-wise A (x of the row staged in xs, BN1 stats
-// of frame t-1 in stat[64..127]).  tile (fused kernel): gE_t also goes into
-// the conv's LDS tile.
+// of frame t-1 in stat[64..127]).
 template <class S, int ACT, int HG>
 __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
                                        int yl, float* wscr, int b, int y, size_t ro,
-                                       const FaIn<S>& in, int lane, S* tile) {
+                                       const FaIn<S>& in, int lane) {
   using F = typename Tr<S>::frag;
   const int c = lane & 31, h = lane >> 5;
   const int t = a.t, T = a.T;
@@ -650,10 +654,6 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
 #pragma unroll
   for (int r = 0; r < 16; ++r) { att[r] = sigm(acc[r] + ba); gEv[r] = att[r] * Ep[r]; }
   store_cl(a.gE + t * fs + ro, c, h, gEv);
-  if (tile) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tile[tile_off<S>(y + PADMAX, cl_x(r, h) + PADMAX, c)] = (S)gEv[r];
-  }
   if (a.gates) {
     const TileLoc tl = tile_loc(b, a.ntx, a.nty);
     const int W = a.ntx * IMG;
@@ -702,7 +702,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
-  fa_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, b, y, ro, in, lane, nullptr);
+  fa_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, b, y, ro, in, lane);
 }
 
 // -------------------------------------------------------------------------
@@ -723,12 +723,11 @@ __device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, size_t ro, int 
   return w;
 }
 
-// One image row of forward point-wise B (BN0 stats of frame t in stat[0..63]);
-// tile (fused kernel): I_t also goes into the conv's LDS tile.
+// One image row of forward point-wise B (BN0 stats of frame t in stat[0..63]).
 template <class S, int ACT, int HG>
 __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
                                        int yl, float* wscr, int y, size_t ro, const FbIn<S>& in,
-                                       int lane, S* tile) {
+                                       int lane) {
   using F = typename Tr<S>::frag;
   const int c = lane & 31, h = lane >> 5;
   const size_t fs = fr_off(1, a.B);
@@ -758,10 +757,6 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, 
     In[r] = (1.f - ig) * (float)in.Iv[r] + ig * ih[r];
   }
   store_cl(a.I + a.t * fs + ro, c, h, In);
-  if (tile) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tile[tile_off<S>(y + PADMAX, cl_x(r, h) + PADMAX, c)] = (S)In[r];
-  }
 }
 
 template <class S, int ACT, int HG>
@@ -793,93 +788,9 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
-  fb_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, y, ro, in, lane, nullptr);
+  fb_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, y, ro, in, lane);
 }
 
-// -------------------------------------------------------------------------
-// Fused forward frame steps (bf16, one 32x32 tile per clip): the point-wise
-// work whose output is a conv's input runs as the conv kernel's prologue in
-// the same workgroup and writes the conv's LDS tile directly (and its HBM copy
-// for the backward), so the conv input is never re-read and a launch per step
-// is saved.  No grid-wide dependency lies between them: the prologue needs the
-// previous conv's BatchNorm statistics, which the launch boundary provides.
-//   k_pw_conv_fa(t): point-wise A (close frame t-1, att, gE_t, eg_t) + conv(gE_t, w_inh)
-//   k_pw_conv_fb(t): point-wise B (BN0, I_t) + conv(I_t, w_exc)
-// The prologue's rows (8 per wave) load their tiles in groups so the loads
-// overlap; its scratch (x rows, transposes, stats) sits above the conv's LDS.
-// Frames made of several tiles keep the separate kernels (the conv halo would
-// need the neighbours' prologue output).
-// -------------------------------------------------------------------------
-template <class S>
-constexpr int fwdx_lds_bytes() {
-  return conv_lds_bytes<S>() + NPIX * 16 /*x rows*/ + NWAVE * SCR_FLOATS * 4 + 128 * 4;
-}
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(NT, 1) void k_pw_conv_fa(ConvArgs<S> ca, CellArgs<S> a) {
-  if constexpr (sizeof(S) == 2) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    f32x4* xs = (f32x4*)(smem + conv_lds_bytes<S>());
-    float* scr = (float*)(xs + NPIX);
-    float* stat = scr + NWAVE * SCR_FLOATS;
-    auto pro = [&](S* tile) {
-      const int t = a.t;
-      // rolling prefetch: G rows' tiles in flight, the first ones under the staging
-      constexpr int G = 4;
-      FaIn<S> in[G];
-#pragma unroll
-      for (int i = 0; i < G; ++i)
-        in[i] = fa_load(a, clip_off(b) + (size_t)(wave * RPW + i) * IMG * C, c, h);
-      stage_x(a.x, a.xu8, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
-      if (t > 0)
-        bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, a.B, a.eps, stat + 64,
-                        b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < RPW; ++j) {
-        const int y = wave * RPW + j;
-        const FaIn<S> cur = in[j % G];
-        if (j + G < RPW)
-          in[j % G] = fa_load(a, clip_off(b) + (size_t)(y + G) * IMG * C, c, h);
-        fa_row<S, ACT, HG>(a, stat, xs, y, scr + wave * SCR_FLOATS, b, y,
-                           clip_off(b) + (size_t)y * IMG * C, cur, lane, tile);
-      }
-    };
-    conv_body<S, FILL_PRO, EPI_FWD>(ca, smem, b, pro);
-  }
-}
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(NT, 1) void k_pw_conv_fb(ConvArgs<S> ca, CellArgs<S> a) {
-  if constexpr (sizeof(S) == 2) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    f32x4* xs = (f32x4*)(smem + conv_lds_bytes<S>());
-    float* scr = (float*)(xs + NPIX);
-    float* stat = scr + NWAVE * SCR_FLOATS;
-    auto pro = [&](S* tile) {
-      const int t = a.t;
-      FbIn<S> in[RPW];                // all 8 rows' tiles in flight under the staging
-#pragma unroll
-      for (int i = 0; i < RPW; ++i)
-        in[i] = fb_load<S, HG>(a, clip_off(b) + (size_t)(wave * RPW + i) * IMG * C, c, h);
-      stage_x(a.x, a.xu8, xs, b, t, a.T, 0, IMG, tid, NT, a.ntx, a.nty);
-      bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, a.B, a.eps, stat,
-                      b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < RPW; ++i) {
-        const int y = wave * RPW + i;
-        fb_row<S, ACT, HG>(a, stat, xs, y, scr + wave * SCR_FLOATS, y,
-                           clip_off(b) + (size_t)y * IMG * C, in[i], lane, tile);
-      }
-    };
-    conv_body<S, FILL_PRO, EPI_FWD>(ca, smem, b, pro);
-  }
-}
 
 // -------------------------------------------------------------------------
 // Backward point-wise A (t from T-1 down to -1).  Two halves:
@@ -890,8 +801,7 @@ __global__ __launch_bounds__(NT, 1) void k_pw_conv_fb(ConvArgs<S> ca, CellArgs<S
 //     (:175, :173) -> d_eg, dc_e (-> BN1 bwd sums), kappa/gamma grads,
 //     dI_t (local), dE_{t-1} partial = (1-eg) dE_t.
 // -------------------------------------------------------------------------
-// Body shared by k_pw_ba (RPP = PWA_RPP rows per wave, PWA_WGPC workgroups per
-// clip) and the fused k_conv_pw_ba (RPP = 8: the conv workgroup's whole clip).
+// Body of k_pw_ba (RPP = PWA_RPP rows per wave, PWA_WGPC workgroups per clip).
 template <class S, int ACT, int HG, int RPP>
 __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int b, int part) {
   using F = typename Tr<S>::frag;
@@ -1031,8 +941,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 template <class S>
 struct BbRow { Pk<S> ginh, Iprev, dep, gEv, dIt, civ; };
 
-// Body shared by k_pw_bb (RPP = 1 row per wave, PWB_WGPC workgroups per clip)
-// and the fused k_conv_pw_bb (RPP = 8: the conv workgroup's whole clip).
+// Body of k_pw_bb (RPP = 1 row per wave, PWB_WGPC workgroups per clip).
 template <class S, int ACT, int HG, int RPP>
 __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int b, int part) {
   using F = typename Tr<S>::frag;
@@ -1200,38 +1109,6 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   pw_bb_body<S, ACT, HG, PWB_RPP>(a, smem, blockIdx.x / PWB_WGPC, blockIdx.x % PWB_WGPC);
 }
 
-// -------------------------------------------------------------------------
-// Fused backward frame steps: the point-wise work that consumes a conv's
-// output runs in the conv's own workgroup (one clip each), right after it,
-// with the LDS re-carved (no grid-wide dependency lies between them: only the
-// BatchNorm-backward sums, which the NEXT launch needs, cross clips).  Saves a
-// launch per step and the re-read of dI_t / dgE from HBM; the point-wise part
-// runs at one wave per SIMD with 8 rows per wave.
-//   k_conv_pw_bb(t): conv^T(BN1-bwd(dcE), w_exc) + adds -> dI_t, then pw_bb(t)
-//   k_conv_pw_ba(t): conv^T(BN0-bwd(dcI), w_inh) + dgEp -> dgE_t (t >= 1; at
-//                    t = 0 only the BN-bwd fill), then pw_ba(t - 1)
-// -------------------------------------------------------------------------
-constexpr int PWX_RPP = IMG / NWAVE;    // 8 rows per wave: the whole clip
-static_assert(NT == PW_NT, "fused kernels run the point-wise bodies with the conv workgroup");
-template <class S>
-constexpr int fused_lds_bytes() {
-  return conv_lds_bytes<S>() > pw_lds_bytes<PWX_RPP, true>() ? conv_lds_bytes<S>()
-                                                              : pw_lds_bytes<PWX_RPP, true>();
-}
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(NT, 1) void k_conv_pw_bb(ConvArgs<S> ca, CellArgs<S> a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL_BNBWD, EPI_ADD>(ca, smem, blockIdx.x);
-  __syncthreads();              // dI_t stores visible to the workgroup; LDS free
-  pw_bb_body<S, ACT, HG, PWX_RPP>(a, smem, blockIdx.x, 0);
-}
-template <class S, int ACT, int HG, int EPI>
-__global__ __launch_bounds__(NT, 1) void k_conv_pw_ba(ConvArgs<S> ca, CellArgs<S> a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL_BNBWD, EPI>(ca, smem, blockIdx.x);
-  __syncthreads();
-  pw_ba_body<S, ACT, HG, PWX_RPP>(a, smem, blockIdx.x, 0);
-}
 
 // D rows per band: 8 (bf16) / 4 (f32, so that two band buffers fit in LDS)
 template <class S> constexpr int wg_rb() { return sizeof(S) == 2 ? 8 : 4; }
@@ -1772,8 +1649,6 @@ void timed(int kind, hipStream_t st, F&& launch) {
   g_tm.ev.emplace_back(a, b);
 }
 
-bool fused_enabled();
-bool fused_fwd_enabled();
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
@@ -1898,17 +1773,6 @@ void launch_pw(K kern, dim3 grid, size_t lds, hipStream_t st, const A& a) {
           : (a.act ? launch_pw(kern<S, 1, 0>, grid, lds, st, a)                  \
                    : launch_pw(kern<S, 0, 0>, grid, lds, st, a)))
 
-// fused conv + point-wise kernels: (activation, cell) -> instantiation
-#define COMMA ,
-template <class K, class CA, class A>
-void launch_fused(K kern, int grid, size_t lds, hipStream_t st, const CA& ca, const A& a) {
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, ca, a);
-}
-#define FUSED_LAUNCH(kern, extra, cargs)                                              \
-  (a.hgru ? (a.act ? launch_fused(kern<S, 1, 1 extra>, p.B, lfu, st, cargs, a)        \
-                   : launch_fused(kern<S, 0, 1 extra>, p.B, lfu, st, cargs, a))       \
-          : (a.act ? launch_fused(kern<S, 1, 0 extra>, p.B, lfu, st, cargs, a)        \
-                   : launch_fused(kern<S, 0, 0 extra>, p.B, lfu, st, cargs, a)))
 
 #define SETLDS(kern, bytes) \
   HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
@@ -1917,9 +1781,9 @@ template <class S>
 int set_lds_attrs() {
   static thread_local bool done = false;   // per host thread; cheap either way
   if (done) return 0;
-  SETLDS((k_conv<S, FILL_COPY, EPI_FWD>), conv_lds_bytes<S>());
-  SETLDS((k_conv<S, FILL_BNBWD, EPI_ADD>), conv_lds_bytes<S>());
-  SETLDS((k_conv<S, FILL_BNBWD, EPI_NONE>), conv_lds_bytes<S>());
+  SETLDS((k_conv_fwd<S>), conv_lds_bytes<S>());
+  SETLDS((k_conv_bwd<S>), conv_lds_bytes<S>());
+  SETLDS((k_bnbwd_fill<S>), conv_lds_bytes<S>());
   SETLDS((k_pw_fa<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 0, 0>), (pw_lds_bytes<PWA_RPP, true>()));
@@ -1937,17 +1801,6 @@ int set_lds_attrs() {
   SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
   SETLDS((k_pw_bb<S, 1, 1>), (pw_lds_bytes<PWB_RPP, true>()));
   SETLDS(k_wgrad<S>, wgrad_lds_bytes<S>());
-#define SETLDS_FUSED(A, H)                                                         \
-  SETLDS((k_conv_pw_bb<S, A, H>), fused_lds_bytes<S>());                           \
-  SETLDS((k_conv_pw_ba<S, A, H, EPI_ADD>), fused_lds_bytes<S>());                  \
-  SETLDS((k_conv_pw_ba<S, A, H, EPI_NONE>), fused_lds_bytes<S>());
-  SETLDS_FUSED(0, 0) SETLDS_FUSED(0, 1) SETLDS_FUSED(1, 0) SETLDS_FUSED(1, 1)
-#undef SETLDS_FUSED
-#define SETLDS_FWDX(A, H)                                                          \
-  SETLDS((k_pw_conv_fa<S, A, H>), fwdx_lds_bytes<S>());                            \
-  SETLDS((k_pw_conv_fb<S, A, H>), fwdx_lds_bytes<S>());
-  SETLDS_FWDX(0, 0) SETLDS_FWDX(0, 1) SETLDS_FWDX(1, 0) SETLDS_FWDX(1, 1)
-#undef SETLDS_FWDX
   done = true;
   return 0;
 }
@@ -1986,28 +1839,19 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
   ca.wf = a.wf_inh;
   cb.wf = a.wf_exc;
-  const bool fx = sizeof(S) == 2 && p.ntx * p.nty == 1 && !d->no_inh && fused_fwd_enabled();
-  const size_t lfu = fwdx_lds_bytes<S>();
-  for (int t = 0; t < p.T && fx; ++t) {
-    a.t = t;
-    ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96;
-    timed(PT_K_FWD_A, st, [&] { FUSED_LAUNCH(k_pw_conv_fa, , ca); });
-    cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * NBNC * 96;
-    timed(PT_K_FWD_B, st, [&] { FUSED_LAUNCH(k_pw_conv_fb, , cb); });
-  }
-  for (int t = fx ? p.T : 0; t <= p.T; ++t) {
+  for (int t = 0; t <= p.T; ++t) {
     a.t = t;
     timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });
     if (t == p.T) break;
     if (!d->no_inh) {
       ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96;
       timed(PT_K_CONV_FA, st, [&] {
-        hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, ca); });
+        hipLaunchKernelGGL((k_conv_fwd<S>), dim3(p.B), dim3(NT), lcv, st, ca); });
     }
     timed(PT_K_PW_FB, st, [&] { PW_LAUNCH(k_pw_fb, gpf, lpf); });
     cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * NBNC * 96;
     timed(PT_K_CONV_FB, st, [&] {
-      hipLaunchKernelGGL((k_conv<S, FILL_COPY, EPI_FWD>), dim3(p.B), dim3(NT), lcv, st, cb); });
+      hipLaunchKernelGGL((k_conv_fwd<S>), dim3(p.B), dim3(NT), lcv, st, cb); });
   }
   if (e_last)
     hipLaunchKernelGGL(k_to_nchw<S>, dim3(256), dim3(256), 0, st,
@@ -2036,38 +1880,14 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   a.t = p.T - 1;
   a.conv_done = 0;
   timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
-  const bool fused = fused_enabled();
-  const size_t lfu = fused_lds_bytes<S>();
-  for (int t = p.T - 1; t >= 0 && fused; --t) {
-    ConvArgs<S> cb = conv_args(a);
-    cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
-    cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
-    cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
-    a.t = t;
-    timed(PT_K_BWD_C, st, [&] { FUSED_LAUNCH(k_conv_pw_bb, , cb); });
-    if (!d->no_inh) {
-      ConvArgs<S> ca = conv_args(a);
-      ca.dc = a.dcI; ca.raw = a.ci + t * fs; ca.bnstat = bst + (size_t)t * 128;
-      ca.bnb = a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64; ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
-      ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
-      a.t = t - 1;
-      a.conv_done = t >= 1;
-      if (t >= 1) timed(PT_K_BWD_D, st, [&] { FUSED_LAUNCH(k_conv_pw_ba, COMMA EPI_ADD, ca); });
-      else timed(PT_K_BWD_D, st, [&] { FUSED_LAUNCH(k_conv_pw_ba, COMMA EPI_NONE, ca); });
-    } else {
-      a.t = t - 1;
-      a.conv_done = 0;
-      timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
-    }
-  }
-  for (int t = p.T - 1; t >= 0 && !fused; --t) {
+  for (int t = p.T - 1; t >= 0; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
     cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
     cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
     cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
     timed(PT_K_CONV_BB, st, [&] {
-      hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_ADD>), dim3(p.B), dim3(NT), lcv, st, cb); });
+      hipLaunchKernelGGL((k_conv_bwd<S>), dim3(p.B), dim3(NT), lcv, st, cb); });
     a.t = t;
     timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
     a.conv_done = 0;
@@ -2079,11 +1899,11 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
       if (t >= 1) {
         timed(PT_K_CONV_BA, st, [&] {
-          hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_ADD>), dim3(p.B), dim3(NT), lcv, st, ca); });
+          hipLaunchKernelGGL((k_conv_bwd<S>), dim3(p.B), dim3(NT), lcv, st, ca); });
         a.conv_done = 1;
       } else {
         timed(PT_K_CONV_BA, st, [&] {
-          hipLaunchKernelGGL((k_conv<S, FILL_BNBWD, EPI_NONE>), dim3(p.B), dim3(NT), lcv, st, ca); });
+          hipLaunchKernelGGL((k_bnbwd_fill<S>), dim3(p.B), dim3(NT), lcv, st, ca); });
       }
     }
     a.t = t - 1;
@@ -2116,27 +1936,6 @@ ptg::GraphCache g_graphs;
 bool use_graph() {
   return ptg::graphs_enabled() && __atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) == 0;
 }
-// PT_CELL_FUSED=1 selects the fused backward frame steps (k_conv_pw_bb /
-// k_conv_pw_ba).  Off by default: measured slower (B=256 T=64 bf16: 119.5 us
-// vs 42 + 66 us for conv_bb + pw_bb, 100 vs 37 + 55 us for conv_ba + pw_ba,
-// 10.0k vs 10.9k clips/s) -- the point-wise half at one wave per SIMD with 8
-// rows per wave exposes its VALU and memory latency that 2 workgroups per CU
-// hide in the separate launches.
-bool fused_enabled() {
-  const char* f = getenv("PT_CELL_FUSED");
-  return f && atoi(f) != 0;
-}
-// PT_CELL_FUSED_FWD=1 selects the fused forward frame steps (k_pw_conv_fa /
-// k_pw_conv_fb; bf16 single-tile frames with an inhibitory conv only).  Off by
-// default for the same reason as the fused backward: measured slower (B=256
-// T=64 bf16: 77 us vs 36 + 34 us for pw_fa + conv_fa, 62 vs 23 + 34 us for
-// pw_fb + conv_fb; 10.3k vs 10.8k clips/s), the prologue's 8 rows per wave at
-// one wave per SIMD expose the latency the 8-workgroup point-wise launches hide,
-// and saving the conv's re-read of its input (3 us of HBM time) cannot pay that.
-bool fused_fwd_enabled() {
-  const char* f = getenv("PT_CELL_FUSED_FWD");
-  return f && atoi(f) != 0;
-}
 int ablate_env() {
   const char* ab = getenv("PT_CELL_ABLATE");
   return ab ? atoi(ab) : 0;
@@ -2168,8 +1967,7 @@ int pt_cell_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* 
   if (!use_graph()) return body(st);
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
-  k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env())
-      .add((int)fused_fwd_enabled());
+  k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 
@@ -2203,8 +2001,7 @@ int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params*
   if (!use_graph()) return body(st);
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
-  k.add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
-      .add((int)fused_enabled());
+  k.add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 
@@ -2241,6 +2038,10 @@ int pt_cell_timing_reset(void) {
 }
 
 const char* pt_last_error(void) { return g_err; }
-const char* pt_version(void) { return "pt_cell 0.1 gfx950"; }
+// PT_SRC_HASH: hash of the sources this library was built from (ptamd/build.py)
+#ifndef PT_SRC_HASH
+#define PT_SRC_HASH "unstamped"
+#endif
+const char* pt_version(void) { return "pt_cell 0.2 gfx950 src " PT_SRC_HASH; }
 
 }  // extern "C"

@@ -999,6 +999,9 @@ int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace
 }
 
 const char* pt_lstm_last_error(void) { return g_err; }
-const char* pt_lstm_version(void) { return "pt_lstm 0.1 gfx950"; }
+#ifndef PT_SRC_HASH
+#define PT_SRC_HASH "unstamped"
+#endif
+const char* pt_lstm_version(void) { return "pt_lstm 0.2 gfx950 src " PT_SRC_HASH; }
 
 }  // extern "C"

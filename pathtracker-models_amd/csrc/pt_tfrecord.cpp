@@ -383,7 +383,9 @@ void decode_file(const std::string& path, const pt_tfr_options& o, FileResult& r
       snprintf(m, sizeof(m), "%s: record %lld length CRC mismatch", path.c_str(), (long long)rec);
       r.msg = m; r.err = PT_TFR_ERR_FORMAT; return;
     }
-    if (raw.size() - off - 12 < len + 4) {
+    // no `len + 4`: a corrupt length near UINT64_MAX would wrap and pass
+    const uint64_t avail = raw.size() - off - 12;
+    if (len > avail || avail - len < 4) {
       snprintf(m, sizeof(m), "%s: truncated record %lld", path.c_str(), (long long)rec);
       r.msg = m; r.err = PT_TFR_ERR_FORMAT; return;
     }

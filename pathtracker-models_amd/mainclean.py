@@ -35,7 +35,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from ptamd.dist import GradBucket, env_rank  # noqa: E402
+from ptamd.dist import GradBucket, env_rank, lockstep  # noqa: E402
 from utils import engine  # noqa: E402
 from utils.earlystopping import EarlyStopping  # noqa: E402
 from utils.misc_functions import AverageMeter, acc_scores  # noqa: E402
@@ -187,7 +187,8 @@ def main(argv=None):
         time_since_last = time.time()
         model.train()
         end = time.perf_counter()
-        for idx, (imgs, target) in enumerate(train_loader):
+        # ranks read different shards: stop all of them at the smallest batch count
+        for idx, (imgs, target) in enumerate(lockstep(train_loader, device)):
             if args.max_iters and idx >= args.max_iters:
                 break
             data_time.update(time.perf_counter() - end)

@@ -9,6 +9,7 @@ box.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -45,6 +46,19 @@ def up_to_date(lib: str = "libptcell.so") -> bool:
     return all(os.path.getmtime(d) <= t for d in srcs + deps)
 
 
+def src_hash(lib: str) -> str:
+    """sha256 (first 12 hex digits) of a library's sources and headers: compiled
+    into its version string, so measurements (profiles/*_pmc_traffic.json) can
+    be matched to the exact kernels that produced them."""
+    h = hashlib.sha256()
+    srcs, deps = LIBS[lib]
+    for f in srcs + deps:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     procs = []
@@ -57,7 +71,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
                    "-pthread", "-Wall", "-I", INC, "-o", out + ".tmp", *srcs, "-lz", "-ldl"]
         else:
             cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                   "-I", INC, "-o", out + ".tmp", *srcs]
+                   f'-DPT_SRC_HASH="{src_hash(lib)}"', "-I", INC, "-o", out + ".tmp", *srcs]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((lib, out, subprocess.Popen(cmd)))

@@ -50,3 +50,30 @@ class GradBucket:
             if p.grad is not None:          # params no rank differentiates stay None
                 p.grad.copy_(self.flat[off:off + n].view_as(p))
             off += n
+
+
+def lockstep(iterable, device):
+    """Yield from a per-rank iterable only while EVERY rank still has an item.
+
+    Each rank reads its own TFRecord shards (file i -> rank i % world), so the
+    ranks' batch counts can differ; a rank that ran out first would leave the
+    loop and meet the others' gradient all-reduce with a different collective.
+    One MIN all-reduce of a has-item flag per step keeps the loop in lockstep:
+    all ranks stop at the smallest count.  Single process: plain iteration.
+    """
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    it = iter(iterable)
+    flag = torch.zeros(1, dtype=torch.int32, device=device)
+    while True:
+        item = next(it, None)
+        if world > 1:
+            flag.fill_(0 if item is None else 1)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                close = getattr(it, "close", None)
+                if close is not None:
+                    close()
+                return
+        elif item is None:
+            return
+        yield item

@@ -86,3 +86,40 @@ def test_two_rank_gradient_average_and_identical_params():
     for k in res[0][1]:
         torch.testing.assert_close(torch.from_numpy(res[0][1][k]), torch.from_numpy(res[1][1][k]),
                                    rtol=0, atol=0)
+
+
+def _lockstep_worker(rank, world, port, out_q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [here, repo, os.path.join(repo, "pathtracker-models_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ptamd.dist import lockstep
+    seen = []
+    # uneven shards: rank r holds 3 + 2 r batches; every step also runs a
+    # collective, as the gradient all-reduce does -- it must never mismatch
+    for item in lockstep(range(3 + 2 * rank), "cpu"):
+        t = torch.tensor([float(item)])
+        dist.all_reduce(t)
+        seen.append((item, float(t)))
+    out_q.put((rank, seen))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_lockstep_stops_all_ranks_at_the_smallest_shard():
+    """mainclean's train loop over per-rank shards with unequal batch counts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lockstep_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(3))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in range(3):
+        assert res[r] == [(i, 3.0 * i) for i in range(3)]

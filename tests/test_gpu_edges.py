@@ -2,19 +2,14 @@
 
 * smallest shapes against the CPU oracle (f32, 1e-3): one clip, one frame;
   an odd batch with two frames; a single-clip 64x64 hGRU (tiles, B=1);
-* the opt-in fused backward (PT_CELL_FUSED=1) against the same oracle;
 * raw u8 clips [B,T,H,W,3] as the cell input (PT_X_U8_NTHWC) against the
   f32 tensor engine.prepare_data builds from them: same values, so logits and
   gradients agree to fp64-atomic summation order (InT f32 / bf16, tiled hGRU);
-* the opt-in fused bf16 forward frame steps (k_pw_conv_fa / k_pw_conv_fb,
-  PT_CELL_FUSED_FWD=1) against the separate launches: same rounding
-  points, so logits and gradients agree to fp64-atomic summation order;
 * at the headline size (B=256, T=64, bf16) where the oracle is too slow:
   permutation equivariance (BatchNorm's batch statistics are symmetric in the
   clips, so permuting the clips permutes the logits; fp64 statistics sums make
   the result order-independent to rounding) and run-to-run reproducibility.
 """
-import os
 
 import numpy as np
 import pytest
@@ -82,45 +77,6 @@ def test_hgru_single_clip_tiled():
     from models import ffhgru_hierarchy as hg
     x, y = _batch(31, 1, 3, hw=64)
     _vs_oracle(_perturbed(hg.FFhGRU, 3, seed=5), x, y, hgru=True)
-
-
-@pytest.mark.parametrize("cell", ["int", "hgru"])
-def test_fused_backward_opt_in(cell):
-    from models import InT, ffhgru_hierarchy as hg
-    x, y = _batch(41, 4, 5)
-    m = _perturbed(hg.FFhGRU if cell == "hgru" else InT.InT, 5, seed=9)
-    os.environ["PT_CELL_FUSED"] = "1"
-    try:
-        _vs_oracle(m, x, y, hgru=cell == "hgru")
-    finally:
-        os.environ.pop("PT_CELL_FUSED")
-
-
-@pytest.mark.parametrize("cell", ["int", "hgru"])
-def test_fused_forward_matches_separate(cell):
-    from models import InT, ffhgru_hierarchy as hg
-    dev = _dev()
-    x, y = _batch(43, 8, 6)
-    m = _perturbed(hg.FFhGRU if cell == "hgru" else InT.InT, 6, seed=11).to(dev)
-    m.cell_dtype = "bf16"
-    x, y = x.to(dev), y.to(dev).reshape(-1, 1)
-    res = []
-    for flag in ("0", "1"):
-        os.environ["PT_CELL_FUSED_FWD"] = flag
-        try:
-            m.zero_grad(set_to_none=True)
-            out, _ = m(x)
-            F.binary_cross_entropy_with_logits(out, y).backward()
-            res.append((out.detach().clone(),
-                        {k: p.grad.detach().clone() for k, p in m.named_parameters()
-                         if p.grad is not None}))
-        finally:
-            os.environ.pop("PT_CELL_FUSED_FWD")
-    (o0, g0), (o1, g1) = res
-    assert torch.isfinite(o1).all()
-    _close("logits", o1, o0, 1e-5)
-    for k in g0:
-        _close(f"grad {k}", g1[k], g0[k], 1e-7, 1e-4)
 
 
 @pytest.mark.parametrize("cell,dtype,hw", [("int", "f32", 32), ("int", "bf16", 32),

@@ -189,3 +189,20 @@ def test_loader_prefetch_thread(tmp_path):
     (bad / "x.tfrecord.gz").write_bytes(gzip.compress(b"\x05\x00\x00\x00\x00\x00\x00\x00junk"))
     with pytest.raises(tfrecord.TFRecordError):
         list(tfr_data_loader(str(bad / "*.gz"), 1, timesteps=T, prefetch=2, pin_memory=False))
+
+
+@pytest.mark.parametrize("verify", [True, False])
+def test_huge_declared_length_is_truncation_not_overread(tmp_path, verify):
+    """A header declaring a length within 4 of UINT64_MAX (length CRC valid)
+    must be reported as a truncated record: `len + 4` would wrap to a small
+    value and let the reader run off the end of the buffer."""
+    import struct
+    for ln in (2 ** 64 - 1, 2 ** 64 - 4, 2 ** 64 - 2, 2 ** 63):
+        hdr = struct.pack("<Q", ln)
+        blob = hdr + struct.pack("<I", ref.masked_crc32c(hdr)) + b"\0" * 32
+        p = str(tmp_path / "huge.tfrecord.gz")
+        with gzip.open(p, "wb") as fh:
+            fh.write(blob)
+        with tfrecord.Reader([p], T, drop_remainder=False, verify_crc=verify) as rd:
+            with pytest.raises(tfrecord.TFRecordError, match="truncated"):
+                list(rd.batches(1))

@@ -11,7 +11,8 @@ columns read from the neighbouring tiles by the conv kernels),
 so the kernels see 4B "tile clips" of bench.py's shape.
 
 Usage:  python tools/bench_hgru.py [--gpus N] [--steps K] [--warmup W]
-        (N>1 under torch.distributed.run, one rank per GPU, as bench.py).
+        (N>1: one rank per GPU over RCCL; started by torch.distributed.run, or
+        launched by this script itself as bench.py does).
 Prints one JSON line; not the headline metric (bench.py is).
 """
 from __future__ import annotations
@@ -85,13 +86,19 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    rc = bench.launch_ranks(sys.argv[1:], args.gpus, script=__file__)
+    if rc is not None:
+        sys.exit(rc)
     from ptamd import _lib
     from ptamd.dist import GradBucket, env_rank
     from models import ffhgru_hierarchy as hg
 
     rank, local_rank, world = env_rank()
+    if world != args.gpus:
+        sys.exit(f"bench_hgru.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        assert dist.get_world_size() == args.gpus
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     torch.manual_seed(1234)

@@ -8,13 +8,21 @@ so fetched bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 is exact for
 fetch_bytes, write_bytes, traffic_bytes}} averaged per launch.
 
 usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [note]
+
+The summary is stamped with the version string of the in-tree libptcell.so
+(it carries the hash of the kernel sources): bench.py only uses a summary whose
+stamp matches the library it runs.
 """
 import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "pathtracker-models_amd"))
 
 
 def _short(name):
@@ -35,7 +43,9 @@ def main():
     fd, wd, out = sys.argv[1:4]
     note = sys.argv[4] if len(sys.argv) > 4 else ""
     fe, wr = _read(fd, "FETCH_SIZE"), _read(wd, "WRITE_SIZE")
-    res = {"note": note, "correction": "fetch_bytes = 2*FETCH_SIZE*1024; write_bytes = WRITE_SIZE*1024",
+    from ptamd import _lib
+    res = {"note": note, "lib_version": _lib.load().pt_version().decode(),
+           "correction": "fetch_bytes = 2*FETCH_SIZE*1024; write_bytes = WRITE_SIZE*1024",
            "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
         f = 2 * 1024 * sum(fe.get(k, [0])) / max(len(fe.get(k, [])), 1)
