@@ -59,7 +59,8 @@ struct CellArgs {
                   // 256 skip the conv epilogue, 512 return at entry (launch floor),
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
                   // atomics, 16 skip the 1x1 weight-gradient LDS reductions,
-                  // 32 skip slab flush
+                  // 32 skip slab flush; precision diagnostics (f32 path only): 2048 round
+                  // the stored E_t to bf16, 4096 the stored I_t, 8192 the stored gE_t, eg_t
   const void* x;                        // f32 [B][3][T][H][W] or u8 [B][T][H][W][3] (xu8)
   int xu8;
   const float *wpre, *bpre;             // [32][3], [32]
@@ -69,7 +70,14 @@ struct CellArgs {
   const F *wf_inh, *wf_exc, *wt_inh, *wt_exc;   // conv fragments (fwd, transposed)
   const F* gf[6];                       // 1x1 fragments, forward
   const F* gt[6];                       // 1x1 fragments, transposed (backward)
-  S *E, *I, *gE, *ci, *ce, *eg;         // saved per frame [T][B][32][32][32]
+  // Saved per frame [T][B][32][32][32].  E is f32 in both modes: stored in
+  // bf16 it stagnates once the excitation settles (|eg (Ehat - E)| below half
+  // a bf16 ulp of E), and the gate gradients, which measure that slow
+  // movement, lost ~25 % of their norm at B=256, T=64 (attention-gate cosine
+  // 0.97 vs the f32 cell; rounding I, gE, eg, c_i or c_e instead moved none of
+  // them below 0.998: tools/bf16_diag2.py).
+  float* E;
+  S *I, *gE, *ci, *ce, *eg;
   S* at;                                // hGRU only: attention map per frame (the gated inhibition)
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
   double* bnacc;                        // fwd BN sums [T][2][NBNC][3][32]: sum mean_b, sum mean_b^2, sum M2_b
@@ -597,16 +605,16 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int 
 //           eg = sig(e_w I_{t-1} + e_u gE) (:171, uses the OLD inhibition;
 //           no_inh: e_w E_{t-1}, :168)
 // -------------------------------------------------------------------------
-template <class S> struct FaIn { Pk<S> Iv, Eo, egv, cev; };
+template <class S> struct FaIn { Pk<S> Iv, egv, cev; f32x16 Eo; };
 template <class S>
 __device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, size_t ro, int c, int h) {
   const size_t fs = fr_off(1, a.B);
   const int t = a.t;
   FaIn<S> w;
-  w.Iv = zero_pk<S>(); w.Eo = zero_pk<S>(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
+  w.Iv = zero_pk<S>(); w.Eo = zero16(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
   if (t > 0) {
     w.Iv = load_pk(a.I + (t - 1) * fs + ro, c, h);
-    if (t >= 2) w.Eo = load_pk(a.E + (t - 2) * fs + ro, c, h);
+    if (t >= 2) w.Eo = load_cl(a.E + (t - 2) * fs + ro, c, h);
     w.egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
     w.cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
   }
@@ -637,8 +645,11 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
       const float cn = A1 * (float)in.cev[r] + B1;
       const float eh = Act<ACT>::f(cn * (kap * (float)in.Iv[r] + gam));
       const float e = (float)in.egv[r];
-      Ep[r] = (1.f - e) * (float)in.Eo[r] + e * eh;
+      Ep[r] = (1.f - e) * in.Eo[r] + e * eh;
     }
+    if (sizeof(S) == 4 && (a.ablate & 2048))
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Ep[r] = (float)(bf16_t)Ep[r];
     store_cl(a.E + (t - 1) * fs + ro, c, h, Ep);
   }
   if (t == T) return;
@@ -653,6 +664,9 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
   f32x16 att, gEv;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { att[r] = sigm(acc[r] + ba); gEv[r] = att[r] * Ep[r]; }
+  if (sizeof(S) == 4 && (a.ablate & 8192))
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gEv[r] = (float)(bf16_t)gEv[r];
   store_cl(a.gE + t * fs + ro, c, h, gEv);
   if (a.gates) {
     const TileLoc tl = tile_loc(b, a.ntx, a.nty);
@@ -678,6 +692,9 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
   f32x16 egn;
 #pragma unroll
   for (int r = 0; r < 16; ++r) egn[r] = sigm(acc[r] + be);
+  if (sizeof(S) == 4 && (a.ablate & 8192))
+#pragma unroll
+    for (int r = 0; r < 16; ++r) egn[r] = (float)(bf16_t)egn[r];
   store_cl(a.eg + t * fs + ro, c, h, egn);
 }
 
@@ -756,6 +773,9 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, 
     const float ig = sigm(acc[r] + bi);
     In[r] = (1.f - ig) * (float)in.Iv[r] + ig * ih[r];
   }
+  if (sizeof(S) == 4 && (a.ablate & 4096))
+#pragma unroll
+    for (int r = 0; r < 16; ++r) In[r] = (float)(bf16_t)In[r];
   store_cl(a.I + a.t * fs + ro, c, h, In);
 }
 
@@ -966,8 +986,9 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
       w.ginh = load_pk(a.at + t * fs + ro, c, h);
       if (t > 0) w.Iprev = load_pk(a.I + (t - 1) * fs + ro, c, h);
     } else {
-      w.ginh = t == 0 ? zero_pk<S>()
-                      : load_pk(a.no_inh ? a.E + (t - 1) * fs + ro : a.I + (t - 1) * fs + ro, c, h);
+      if (t == 0) w.ginh = zero_pk<S>();
+      else if (a.no_inh) w.ginh = to_pk<S>(load_cl(a.E + (t - 1) * fs + ro, c, h));
+      else w.ginh = load_pk(a.I + (t - 1) * fs + ro, c, h);
     }
     w.dep = load_pk(a.dEp + ro, c, h);
     w.gEv = load_pk(a.gE + t * fs + ro, c, h);
@@ -1691,7 +1712,7 @@ Plan plan(const pt_cell_desc* d) {
   p.frame = (size_t)p.B * NPIX * C;
   const size_t fbytes = al(p.frame * p.T * p.es);
   size_t o = 0;
-  p.o_E = o; o += fbytes;
+  p.o_E = o; o += al(p.frame * p.T * 4);          // f32 in both modes (CellArgs::E)
   p.o_I = o; o += fbytes;
   p.o_gE = o; o += fbytes;
   p.o_ci = o; o += fbytes;
@@ -1739,7 +1760,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
     a.gf[i] = (const F*)(saved + p.o_g[i]);
     a.gt[i] = (const F*)(saved + p.o_g[6 + i]);
   }
-  a.E = (S*)(saved + p.o_E); a.I = (S*)(saved + p.o_I); a.gE = (S*)(saved + p.o_gE);
+  a.E = (float*)(saved + p.o_E); a.I = (S*)(saved + p.o_I); a.gE = (S*)(saved + p.o_gE);
   a.ci = (S*)(saved + p.o_ci); a.ce = (S*)(saved + p.o_ce); a.eg = (S*)(saved + p.o_eg);
   a.at = a.hgru ? (S*)(saved + p.o_at) : nullptr;
   a.bnstat = (float*)(saved + p.o_bnstat);
@@ -1854,8 +1875,8 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
       hipLaunchKernelGGL((k_conv_fwd<S>), dim3(p.B), dim3(NT), lcv, st, cb); });
   }
   if (e_last)
-    hipLaunchKernelGGL(k_to_nchw<S>, dim3(256), dim3(256), 0, st,
-                       (const S*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0, p.ntx, p.nty);
+    hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, st,
+                       (const float*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0, p.ntx, p.nty);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1976,12 +1997,9 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, p
   if (!saved || !e_seq) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
   const Plan p = plan(d);
   for (int t = 0; t < p.T; ++t) {
-    if (d->dtype == PT_DTYPE_BF16)
-      hipLaunchKernelGGL(k_to_nchw<bf16_t>, dim3(256), dim3(256), 0, (hipStream_t)stream,
-                         (const bf16_t*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B, p.T, t, p.ntx, p.nty);
-    else
-      hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, (hipStream_t)stream,
-                         (const float*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B, p.T, t, p.ntx, p.nty);
+    hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, (hipStream_t)stream,   // E is f32
+                       (const float*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B,
+                       p.T, t, p.ntx, p.nty);
   }
   HIPCHK(hipGetLastError());
   return 0;

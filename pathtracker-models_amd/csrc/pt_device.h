@@ -108,6 +108,12 @@ __device__ __forceinline__ Pk<S> load_pk(const S* __restrict__ row, int c, int h
   for (int r = 0; r < 16; ++r) v[r] = row[cl_x(r, h) * C + c];
   return v;
 }
+template <class S> __device__ __forceinline__ Pk<S> to_pk(const f32x16& v) {
+  Pk<S> o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = (S)v[r];
+  return o;
+}
 template <class S> __device__ __forceinline__ Pk<S> zero_pk() {
   Pk<S> v;
 #pragma unroll
