@@ -484,6 +484,7 @@ constexpr int pw_lds_bytes() {   // forward point-wise kernels use xs, scr, stat
                    PW_NGACC * 1024 * 4 /*gacc*/ + SLAB * 4 /*slab copy*/;
 }
 struct PLds {
+  bf16x8* stage;  // k_pw_bb, bf16: [3 slots][PW_NW waves][2 k-steps][64 lanes] wgrad operands
   f32x4* xs;
   float* scr;     // [PW_NW][SCR_FLOATS]
   float* stat;    // [128]
@@ -505,6 +506,68 @@ __device__ __forceinline__ PLds pcarve(char* smem) {
   l.flush = l.scr;       // gacc_row runs between a wave's transposes, fenced by barriers
   l.slabl = l.gacc + PW_NGACC * 1024;
   return l;
+}
+
+// k_pw_bb's layout.  bf16: the 1x1 weight gradients are formed by one wave
+// per gate from operands the four waves stage in LDS (stage_wg / gate_wgrad
+// below) instead of the per-row gacc reductions; the slab copy holds only the
+// fields this kernel updates (gate tiles 2..5 and the per-channel block:
+// slab offsets from 2 * 1024), slabl points 2048 floats before it.
+constexpr int PWB_STAGE_SLOTS = 3;
+constexpr int PWB_SLAB_LO = 2 * 1024;
+template <class S>
+constexpr int pwb_lds_bytes() {
+  return PW_NW * PWB_RPP * IMG * 16 /*xs*/ + PW_NW * SCR_FLOATS * 4 /*scr*/ + 128 * 4 /*stat*/ +
+         PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ +
+         (sizeof(S) == 2 ? PWB_STAGE_SLOTS * PW_NW * 2 * 64 * 16 : PW_NGACC * 1024 * 4) +
+         (SLAB - PWB_SLAB_LO) * 4 /*slab copy*/;
+}
+template <class S>
+__device__ __forceinline__ PLds pcarve_bb(char* smem) {
+  PLds l = pcarve<PWB_RPP>(smem);
+  char* p = (char*)(l.red + 512);
+  if constexpr (sizeof(S) == 2) {
+    l.stage = (bf16x8*)p;
+    l.gacc = nullptr;
+    p += PWB_STAGE_SLOTS * PW_NW * 2 * 64 * 16;
+  } else {
+    l.stage = nullptr;
+    l.gacc = (float*)p;
+    p += PW_NGACC * 1024 * 4;
+  }
+  l.slabl = (float*)p - PWB_SLAB_LO;
+  return l;
+}
+// bf16 1x1 weight gradients without the per-row cross-wave reductions: every
+// wave parks its row's operand tile (CL registers packed as the bf16 MFMA
+// fragments of wgrad_cl) in a slot; after a barrier ONE wave contracts the
+// four rows of its gate (8 MFMAs, k = 128 pixels) and adds the tile into the
+// workgroup's slab (slabl holds the prefetched old values).
+template <class V>
+__device__ __forceinline__ void stage_wg(bf16x8* stage, int slot, const V& v, int wave, int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (bf16_t)(float)v[8 * s + j];
+    stage[((slot * PW_NW + wave) * 2 + s) * 64 + lane] = f;
+  }
+}
+__device__ __forceinline__ void gate_wgrad(const bf16x8* stage, int dslot, int xslot, int g,
+                                           const float* slabl, float* slab_p, int lane) {
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int w = 0; w < PW_NW; ++w)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      acc = Tr<bf16_t>::mma(stage[((dslot * PW_NW + w) * 2 + s) * 64 + lane],
+                            stage[((xslot * PW_NW + w) * 2 + s) * 64 + lane], acc);
+  const int ci = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int o = g * 1024 + cl_x(r, h) * 32 + ci;
+    slab_p[o] = slabl[o] + acc[r];
+  }
 }
 
 // Add one row's 1x1 weight-gradient tile (dW[n][ci] = sum_p D[p][n] X[p][ci],
@@ -965,7 +1028,8 @@ struct BbRow { Pk<S> ginh, Iprev, dep, gEv, dIt, civ; };
 template <class S, int ACT, int HG, int RPP>
 __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int b, int part) {
   using F = typename Tr<S>::frag;
-  const PLds L = pcarve<RPP>(smem);
+  constexpr bool BF = sizeof(S) == 2;      // staged wave-per-gate 1x1 weight gradients
+  const PLds L = pcarve_bb<S>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = a.t, T = a.T, B = a.B;
@@ -1005,7 +1069,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   if constexpr (RPP == 1) pre = load_row(clip_off(b) + (size_t)(y0 + wave) * IMG * C);
   slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);        // i_w, i_u, e_w, e_u
   stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
-  gacc_zero(L.gacc, 4, tid);
+  if constexpr (!BF) gacc_zero(L.gacc, 4, tid);
   __syncthreads();
 
   const float* bs = a.bnstat + (size_t)t * 128;
@@ -1034,8 +1098,18 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
       f32x16 depf;
 #pragma unroll
       for (int r = 0; r < 16; ++r) depf[r] = (float)w.dep[r];
-      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
-      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, w.gEv, lane, wave, tid);
+      if constexpr (BF) {
+        // slots: 0 d_e_pre, 1 g_inh, 2 gE_t; waves 0 / 1 form e_w / e_u (slab gates 4, 5)
+        stage_wg(L.stage, 0, depf, wave, lane);
+        stage_wg(L.stage, 1, ginh, wave, lane);
+        stage_wg(L.stage, 2, w.gEv, wave, lane);
+        __syncthreads();
+        if (wave < 2 && !(a.ablate & 16))
+          gate_wgrad(L.stage, 0, 1 + wave, 4 + wave, L.slabl, slab_p, lane);
+      } else {
+        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
+        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, w.gEv, lane, wave, tid);
+      }
       sm[3] += hsum16(depf);
       cl_to_pa<S>(wscr, depf, lane, pe);
       const f32x16 dIt0 = a.no_inh ? load_cl(a.dIt + ro, c, h) : zero16();
@@ -1089,8 +1163,19 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         bs0 += dci;
         bs1 += dci * xi;
       }
-      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
-      if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
+      if constexpr (BF) {
+        // slots 0 / 2 are free once waves 0 / 1 have read them: d_i_pre -> 0, x -> 2;
+        // waves 2 / 3 form i_w (x) / i_u (g_inh) (slab gates 2, 3)
+        __syncthreads();
+        stage_wg(L.stage, 0, dip, wave, lane);
+        stage_wg(L.stage, 2, xv, wave, lane);
+        __syncthreads();
+        if (wave >= 2 && !(a.ablate & 16))
+          gate_wgrad(L.stage, 0, wave == 2 ? 2 : 1, wave, L.slabl, slab_p, lane);
+      } else {
+        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
+        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
+      }
       F pd[Tr<S>::KS];
       cl_to_pa<S>(wscr, dip, lane, pd);
       dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
@@ -1119,9 +1204,11 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   if (!a.no_inh && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64, lane, wave, tid);
   if (a.ablate & 32) return;
   flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
-  // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5
-  if (!a.no_inh) gacc_flush(L.gacc, L.slabl, slab_p, 2, 2, tid);
-  gacc_flush(L.gacc + 2 * 1024, L.slabl, slab_p, 4, 2, tid);
+  // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5 (bf16: written by gate_wgrad)
+  if constexpr (!BF) {
+    if (!a.no_inh) gacc_flush(L.gacc, L.slabl, slab_p, 2, 2, tid);
+    gacc_flush(L.gacc + 2 * 1024, L.slabl, slab_p, 4, 2, tid);
+  }
 }
 template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
@@ -1808,19 +1895,19 @@ int set_lds_attrs() {
   SETLDS((k_pw_fa<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 0, 0>), (pw_lds_bytes<PWA_RPP, true>()));
-  SETLDS((k_pw_bb<S, 0, 0>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_bb<S, 0, 0>), (pwb_lds_bytes<S>()));
   SETLDS((k_pw_fa<S, 0, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 0, 1>), (pw_lds_bytes<PWA_RPP, true>()));
-  SETLDS((k_pw_bb<S, 0, 1>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_bb<S, 0, 1>), (pwb_lds_bytes<S>()));
   SETLDS((k_pw_fa<S, 1, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 1, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 1, 0>), (pw_lds_bytes<PWA_RPP, true>()));
-  SETLDS((k_pw_bb<S, 1, 0>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_bb<S, 1, 0>), (pwb_lds_bytes<S>()));
   SETLDS((k_pw_fa<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
-  SETLDS((k_pw_bb<S, 1, 1>), (pw_lds_bytes<PWB_RPP, true>()));
+  SETLDS((k_pw_bb<S, 1, 1>), (pwb_lds_bytes<S>()));
   SETLDS(k_wgrad<S>, wgrad_lds_bytes<S>());
   done = true;
   return 0;
@@ -1894,7 +1981,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
-  const size_t lpa = (pw_lds_bytes<PWA_RPP, true>()), lpb = (pw_lds_bytes<PWB_RPP, true>());
+  const size_t lpa = (pw_lds_bytes<PWA_RPP, true>()), lpb = pwb_lds_bytes<S>();
   const size_t lcv = conv_lds_bytes<S>();
   const size_t fs = p.frame;
   const float* bst = a.bnstat;

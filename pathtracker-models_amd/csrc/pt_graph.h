@@ -64,7 +64,7 @@ class GraphCache {
       const hipError_t ei = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
       (void)hipGraphDestroy(g);
       if (ei != hipSuccess) return hip_err;
-      insert(key, nkey, dev, exec);
+      exec = insert(key, nkey, dev, exec);     // another thread may have won the race
     }
     return hipGraphLaunch(exec, st) == hipSuccess ? 0 : hip_err;
   }
@@ -89,8 +89,16 @@ class GraphCache {
       }
     return nullptr;
   }
-  void insert(const void* key, size_t n, int dev, hipGraphExec_t exec) {
+  // Returns the exec to launch: `exec`, or the entry another thread inserted
+  // for the same key meanwhile (then `exec` is destroyed: it never launched).
+  hipGraphExec_t insert(const void* key, size_t n, int dev, hipGraphExec_t exec) {
     std::lock_guard<std::mutex> lk(mu_);
+    for (auto& x : e_)
+      if (x.dev == dev && x.key.size() == n && memcmp(x.key.data(), key, n) == 0) {
+        (void)hipGraphExecDestroy(exec);
+        x.used = ++tick_;
+        return x.exec;
+      }
     if (e_.size() >= CAP) {
       size_t lru = 0;
       for (size_t i = 1; i < e_.size(); ++i)
@@ -107,6 +115,7 @@ class GraphCache {
     x.exec = exec;
     x.used = ++tick_;
     e_.push_back(std::move(x));
+    return exec;
   }
 };
 

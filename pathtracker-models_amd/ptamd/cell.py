@@ -10,6 +10,7 @@ BPTT through it (mainclean.py:204).
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -79,6 +80,26 @@ def _desc(cfg: CellConfig, x: torch.Tensor, channels: int) -> _lib.Desc:
                      x_format=_lib.PT_X_U8_NTHWC if x.dtype == torch.uint8 else _lib.PT_X_F32_NCTHW)
 
 
+# f32 contiguous staging copies of parameters that are not (e.g. a model moved
+# to another dtype): one persistent buffer per parameter, refreshed in place
+# each call, so the device pointers -- and with them the library's cached
+# hipGraph (pt_graph.h, keyed by every pointer) -- stay the same from step to
+# step instead of a fresh temporary forcing a re-capture per call.
+_STAGED = weakref.WeakKeyDictionary()
+
+
+def _as_f32(p):
+    if p is None or (p.dtype == torch.float32 and p.is_contiguous()):
+        return p
+    buf = _STAGED.get(p)
+    if buf is None or buf.shape != p.shape or buf.device != p.device:
+        buf = torch.empty(p.shape, dtype=torch.float32, device=p.device)
+        _STAGED[p] = buf
+    with torch.no_grad():
+        buf.copy_(p)
+    return buf
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
@@ -120,7 +141,7 @@ class RecurrentCellFn(torch.autograd.Function):
         _require_device(x)
         lib = _lib.load()
         x = x.contiguous() if x.dtype == torch.uint8 else x.contiguous().float()
-        params = [p.contiguous().float() if p is not None else None for p in params]
+        params = [_as_f32(p) for p in params]
         c = params[0].shape[0]
         d = _desc(cfg, x, c)
         saved = torch.empty(lib.pt_cell_saved_bytes(ctypes.byref(d)), dtype=torch.uint8,
