@@ -49,11 +49,13 @@ enum { PT_X_F32_NCTHW = 0, PT_X_U8_NTHWC = 1 };
 /* Problem description. */
 typedef struct pt_cell_desc {
     int32_t batch;      /* B  clips on this device                              */
-    int32_t channels;   /* C  = `dimensions` (utils/engine.py:75); must be 32  */
+    int32_t channels;   /* C  = `dimensions` (utils/engine.py:75); 1..32: C < 32
+                           runs zero-padded to the 32-wide MFMA tile          */
     int32_t frames;     /* T  = x.shape[2]                                      */
     int32_t height;     /* H  multiple of 32 (32; 64 for hGRU cfg4)             */
     int32_t width;      /* W  multiple of 32; frames > 32x32 run as 32x32 tiles */
-    int32_t ksize;      /* horizontal kernel size, odd, <= 7 (engine default 7) */
+    int32_t ksize;      /* horizontal kernel size, odd, <= 15 (engine passes 7;
+                           the constructors' default is 15)                  */
     int32_t act;        /* PT_ACT_*                                             */
     int32_t no_inh;     /* InT_no_inh (models/InT.py:168)                       */
     int32_t cell;       /* PT_CELL_*                                            */

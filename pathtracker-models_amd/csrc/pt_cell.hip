@@ -50,6 +50,7 @@ template <class S>
 struct CellArgs {
   using F = typename Tr<S>::frag;
   int B, T, K, act, no_inh;
+  int Cu;         // the caller's channel count (<= 32; the kernels run 32, padded, see k_pad_params)
   int hgru;       // hConvGRUCell: the gated inhibition is the attention map (ffhgru_hierarchy.py:147)
   float eps;
   int t;
@@ -150,37 +151,43 @@ __device__ void stage_x(const void* __restrict__ xv, int xu8, f32x4* xs, int v, 
 // right) are channel chunks of the neighbouring tiles (ld maps a chunk's
 // element offset to its 16 B, e.g. applying BatchNorm backward); positions
 // outside the frame keep the zeros of tile_zero.
-template <class S, class Ld>
+template <class S, int PAD, class Ld>
 __device__ __forceinline__ void tile_halo(S* __restrict__ tile, int v, int ntx, int nty, int pass,
                                           int tid, Ld&& ld) {
   constexpr int CPB = 16 / (int)sizeof(S);
   constexpr int NCH = Tr<S>::CP / CPB;
-  constexpr int NHP = TILE * TILE - NPIX;              // 420
+  constexpr int TW = tile_w<PAD>();
+  constexpr int NHP = TW * TW - NPIX;                  // 420 (PAD 3) / 1092 (PAD 7)
   constexpr int PER = (NHP * NCH + NT - 1) / NT;
+  constexpr int BATCH = 6;                             // loads in flight per thread
   const TileLoc L = tile_loc(v, ntx, nty);
-  u32x4 val[PER];
-  int dst[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int idx = tid + k * NT;
-    const int hp = idx / NCH, q = idx - hp * NCH;
-    int hy, hx;
-    if (hp < 3 * TILE) { hy = hp / TILE - PADMAX; hx = hp % TILE - PADMAX; }
-    else if (hp < 6 * TILE) { const int j = hp - 3 * TILE; hy = IMG + j / TILE; hx = j % TILE - PADMAX; }
-    else if (hp < 6 * TILE + 3 * IMG) { const int j = hp - 6 * TILE; hy = j / 3; hx = j % 3 - PADMAX; }
-    else { const int j = hp - 6 * TILE - 3 * IMG; hy = j / 3; hx = IMG + j % 3; }
-    const int dy = hy < 0 ? -1 : (hy >= IMG ? 1 : 0), dx = hx < 0 ? -1 : (hx >= IMG ? 1 : 0);
-    const bool ok = idx < NHP * NCH && L.ty + dy >= 0 && L.ty + dy < nty && L.tx + dx >= 0 &&
-                    L.tx + dx < ntx;
-    const int ly = hy - dy * IMG, lx = hx - dx * IMG;
-    const size_t e = clip_off(ok ? v + dy * ntx + dx : v) + (size_t)(ly * IMG + lx) * C +
-                     pass * Tr<S>::CP + q * CPB;
-    val[k] = ld(ok ? e : clip_off(v), pass * Tr<S>::CP + q * CPB);
-    dst[k] = ok ? tile_off<S>(hy + PADMAX, hx + PADMAX, q * CPB) : -1;
+  for (int k0 = 0; k0 < PER; k0 += BATCH) {
+    u32x4 val[BATCH];
+    int dst[BATCH];
+#pragma unroll
+    for (int kk = 0; kk < BATCH; ++kk) {
+      const int k = k0 + kk;
+      const int idx = tid + k * NT;
+      const int hp = idx / NCH, q = idx - hp * NCH;
+      int hy, hx;
+      if (hp < PAD * TW) { hy = hp / TW - PAD; hx = hp % TW - PAD; }
+      else if (hp < 2 * PAD * TW) { const int j = hp - PAD * TW; hy = IMG + j / TW; hx = j % TW - PAD; }
+      else if (hp < 2 * PAD * TW + PAD * IMG) { const int j = hp - 2 * PAD * TW; hy = j / PAD; hx = j % PAD - PAD; }
+      else { const int j = hp - 2 * PAD * TW - PAD * IMG; hy = j / PAD; hx = IMG + j % PAD; }
+      const int dy = hy < 0 ? -1 : (hy >= IMG ? 1 : 0), dx = hx < 0 ? -1 : (hx >= IMG ? 1 : 0);
+      const bool ok = k < PER && idx < NHP * NCH && L.ty + dy >= 0 && L.ty + dy < nty &&
+                      L.tx + dx >= 0 && L.tx + dx < ntx;
+      const int ly = hy - dy * IMG, lx = hx - dx * IMG;
+      const size_t e = clip_off(ok ? v + dy * ntx + dx : v) + (size_t)(ly * IMG + lx) * C +
+                       pass * Tr<S>::CP + q * CPB;
+      val[kk] = ld(ok ? e : clip_off(v), pass * Tr<S>::CP + q * CPB);
+      dst[kk] = ok ? tile_off<S, PAD>(hy + PAD, hx + PAD, q * CPB) : -1;
+    }
+#pragma unroll
+    for (int kk = 0; kk < BATCH; ++kk)
+      if (dst[kk] >= 0) *(u32x4*)(tile + dst[kk]) = val[kk];
   }
-#pragma unroll
-  for (int k = 0; k < PER; ++k)
-    if (dst[k] >= 0) *(u32x4*)(tile + dst[k]) = val[k];
 }
 
 // Stem (models/InT.py:212-213): z = W_pre x + b; xbn = nl(z); CL layout.
@@ -296,8 +303,11 @@ struct ConvArgs {
 };
 
 constexpr int CONV_MISC = 512;  // floats: red[256] (bn-bwd table [3][32] aliases it)
-template <class S>
-constexpr int conv_lds_bytes() { return tile_bytes<S>() + CONV_MISC * 4 + 2 * WSLICE_BYTES; }
+// k <= 7: 38 x 38 tile + two weight slices; k > 7: 46 x 46 tile, weights from L2
+template <class S, int PAD = PADMAX>
+constexpr int conv_lds_bytes() {
+  return tile_bytes<S, PAD>() + CONV_MISC * 4 + (PAD == PADMAX ? 2 * WSLICE_BYTES : 0);
+}
 
 // conv_run row hook of EPI_FWD: store a finished output row (PL layout)
 template <class S>
@@ -310,10 +320,10 @@ struct StoreRow {
   }
 };
 
-template <class S, int FILL, int EPI>
+template <class S, int FILL, int EPI, int PAD>
 __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b) {
   S* tile = (S*)smem;
-  float* red = (float*)(smem + tile_bytes<S>());
+  float* red = (float*)(smem + tile_bytes<S, PAD>());
   float* tbl = red + 128;       // FILL_BNBWD: per-channel A, Bc, Cc
   char* wbuf = (char*)(red + CONV_MISC);   // 2 weight slices
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
@@ -336,7 +346,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       tbl[64 + tid] = -A * md + A * mdx * rstd * mean;
     }
   }
-  if constexpr (EPI != EPI_NONE) tile_zero<S>(tile, tid);
+  if constexpr (EPI != EPI_NONE) tile_zero<S, PAD>(tile, tid);
   __syncthreads();
 
   const bool tiled = a.ntx * a.nty > 1;
@@ -356,12 +366,12 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
   auto fill = [&](int pass) {
     if constexpr (FILL == FILL_COPY) {
       if (tiled)
-        tile_halo<S>(tile, b, a.ntx, a.nty, pass, tid,
-                     [&](size_t e, int) { return *(const u32x4*)(a.src + e); });
-      tile_fill<S>(tile, a.src + cb, pass, tid);
+        tile_halo<S, PAD>(tile, b, a.ntx, a.nty, pass, tid,
+                          [&](size_t e, int) { return *(const u32x4*)(a.src + e); });
+      tile_fill<S, PAD>(tile, a.src + cb, pass, tid);
     } else if constexpr (FILL == FILL_BNBWD) {
       if (EPI != EPI_NONE && tiled)
-        tile_halo<S>(tile, b, a.ntx, a.nty, pass, tid, [&](size_t e, int ch0) {
+        tile_halo<S, PAD>(tile, b, a.ntx, a.nty, pass, tid, [&](size_t e, int ch0) {
           return bnbwd16(*(const u32x4*)(a.dc + e), *(const u32x4*)(a.raw + e), ch0);
         });
       constexpr int CPB = 16 / (int)sizeof(S);      // channels per 16-B chunk of S
@@ -397,7 +407,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
           *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
           if constexpr (EPI != EPI_NONE) {
             const int y = pix >> 5, x = pix & 31;
-            *(uint4*)(tile + tile_off<S>(y + PADMAX, x + PADMAX, q * CPB)) = ov;
+            *(uint4*)(tile + tile_off<S, PAD>(y + PAD, x + PAD, q * CPB)) = ov;
           }
         }
       }
@@ -416,11 +426,11 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       // each finished row is stored while the later rows' MFMAs still run
       // (all 256 workgroups storing at the very end took ~6.5 us per launch)
       const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RPW) * IMG + px) * C, h};
-      conv_run<S>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate, sr);
+      conv_run<S, PAD>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate, sr);
       if (a.ablate & 256) return;
       if (!(a.ablate & 8)) bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
     } else {
-      conv_run<S>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate);
+      conv_run<S, PAD>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate);
       if (a.ablate & 256) return;
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
@@ -435,20 +445,20 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
   }
 }
 // Distinct kernel names per role (rocprof summaries tell them apart).
-template <class S>
+template <class S, int PAD>
 __global__ __launch_bounds__(NT, 1) void k_conv_fwd(ConvArgs<S> a) {     // conv + BN partials
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL_COPY, EPI_FWD>(a, smem, blockIdx.x);
+  conv_body<S, FILL_COPY, EPI_FWD, PAD>(a, smem, blockIdx.x);
 }
-template <class S>
+template <class S, int PAD>
 __global__ __launch_bounds__(NT, 1) void k_conv_bwd(ConvArgs<S> a) {     // BN bwd + conv^T + adds
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL_BNBWD, EPI_ADD>(a, smem, blockIdx.x);
+  conv_body<S, FILL_BNBWD, EPI_ADD, PAD>(a, smem, blockIdx.x);
 }
 template <class S>
 __global__ __launch_bounds__(NT, 1) void k_bnbwd_fill(ConvArgs<S> a) {   // frame 0: BN bwd only
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL_BNBWD, EPI_NONE>(a, smem, blockIdx.x);
+  conv_body<S, FILL_BNBWD, EPI_NONE, PADMAX>(a, smem, blockIdx.x);
 }
 
 // =========================================================================
@@ -731,10 +741,10 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) gEv[r] = (float)(bf16_t)gEv[r];
   store_cl(a.gE + t * fs + ro, c, h, gEv);
-  if (a.gates) {
+  if (a.gates && c < a.Cu) {
     const TileLoc tl = tile_loc(b, a.ntx, a.nty);
     const int W = a.ntx * IMG;
-    float* gp = a.gates + (((size_t)tl.b * T + t) * C + c) * ((size_t)a.nty * IMG * W) +
+    float* gp = a.gates + (((size_t)tl.b * T + t) * a.Cu + c) * ((size_t)a.nty * IMG * W) +
                 (size_t)(tl.ty * IMG + y) * W + tl.tx * IMG;
 #pragma unroll
     for (int r = 0; r < 16; ++r) gp[cl_x(r, h)] = att[r];
@@ -1218,19 +1228,39 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
 }
 
 
-// D rows per band: 8 (bf16) / 4 (f32, so that two band buffers fit in LDS)
-template <class S> constexpr int wg_rb() { return sizeof(S) == 2 ? 8 : 4; }
-template <class S> constexpr int wg_xr() { return wg_rb<S>() + 2 * PADMAX; }
-constexpr int WG_NACC = 13;            // taps per wave: wave + 4 m, m < 13
-template <class S>
-constexpr int wgrad_band_elems() { return wg_xr<S>() * TILE * C + wg_rb<S>() * IMG * C; }
-template <class S>
-constexpr int wgrad_lds_bytes() { return 2 * wgrad_band_elems<S>() * (int)sizeof(S); }  // 2 buffers
+// Band geometry by halo width PAD (k <= 7: 3, k > 7: 7): D rows per band (so
+// that the band buffers fit in LDS) and buffers (2 = double-buffered; f32 at
+// PAD 7 has room for one).
+template <class S, int PAD> constexpr int wg_rb() {
+  return sizeof(S) == 2 ? (PAD == PADMAX ? 8 : 4) : (PAD == PADMAX ? 4 : 2);
+}
+template <class S, int PAD> constexpr int wg_nbuf() { return sizeof(S) == 4 && PAD != PADMAX ? 1 : 2; }
+template <class S, int PAD> constexpr int wg_xr() { return wg_rb<S, PAD>() + 2 * PAD; }
+constexpr int WG_NACC = 13;            // f32: accumulator tiles per wave (taps tap0 + wave + 4 m)
+// f32 taps per wave and group actually used: 13 at PAD 3 (49 taps, one
+// group); 8 at PAD 7 (the single-buffered band needs the registers)
+template <int PAD> constexpr int wg_nacc() { return PAD == PADMAX ? WG_NACC : 8; }
+template <class S, int PAD>
+constexpr int wgrad_band_elems() {
+  return wg_xr<S, PAD>() * tile_w<PAD>() * C + wg_rb<S, PAD>() * IMG * C;
+}
+template <class S, int PAD>
+constexpr int wgrad_lds_bytes() {
+  return wg_nbuf<S, PAD>() * wgrad_band_elems<S, PAD>() * (int)sizeof(S);
+}
+// Tap groups (grid.z): the accumulator tiles of one pass cover at most 7 x 8
+// taps (bf16: 7 kernel rows x 2 columns per wave) / 52 taps (f32); k > 7
+// makes several passes over the data, one per group.
+inline int wgrad_groups(int K, bool bf16) {
+  if (K <= 2 * PADMAX + 1) return 1;
+  return bf16 ? ((K + 6) / 7) * ((K + 7) / 8) : (K * K + 4 * wg_nacc<PADBIG>() - 1) / (4 * wg_nacc<PADBIG>());
+}
 
 // Unswizzled channels-last band images: the transposed 4x16 block reads
 // (ds_read_b64_tr_b16) and the f32 row reads are bank-conflict free on them,
 // and every tap is a constant element offset from a per-lane base.
-__device__ __forceinline__ int wx_off(int row, int col, int ch) { return (row * TILE + col) * C + ch; }
+template <int PAD>
+__device__ __forceinline__ int wx_off(int row, int col, int ch) { return (row * tile_w<PAD>() + col) * C + ch; }
 __device__ __forceinline__ int wd_off(int row, int col, int ch) { return (row * IMG + col) * C + ch; }
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -1241,19 +1271,21 @@ __device__ __forceinline__ bf16x8 tr_read8(const bf16_t* p) {
   return __builtin_shufflevector(tr_read(p), tr_read(p + 4 * C), 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// One band = (frame, clip, 8 D rows): the X rows y0-3 .. y0+10 (interior
-// columns; the 3 halo columns each side stay zero from the initial clear,
-// rows outside the image are written as zeros) and the 8 D rows.
-template <class S>
+// One band = (frame, clip, RB D rows): the X rows y0-PAD .. y0+RB-1+PAD
+// (interior columns; the PAD halo columns each side stay zero from the
+// initial clear, rows outside the image are written as zeros) and the D rows.
+template <class S, int PAD>
 struct WBand {
   static constexpr int CPB = 16 / (int)sizeof(S);
   static constexpr int NCH = C / CPB;
-  static constexpr int XPER = wg_xr<S>() * IMG * NCH / NT;     // 7 (bf16) / 14 (f32)
-  static constexpr int DPER = wg_rb<S>() * IMG * NCH / NT;     // 4 / 8
-  // tiled frames only: the 6 halo columns of the X rows come from the left /
+  static constexpr int RB = wg_rb<S, PAD>(), XR = wg_xr<S, PAD>();
+  static constexpr int XPER = XR * IMG * NCH / NT;     // 7 / 10 (PAD 3), 9 / 16 (PAD 7)
+  static constexpr int DPER = RB * IMG * NCH / NT;     // 4 / 4, 2 / 2
+  static_assert(XR * IMG * NCH % NT == 0 && RB * IMG * NCH % NT == 0, "band split");
+  // tiled frames only: the 2 PAD halo columns of the X rows come from the left /
   // right neighbour tiles (at 32x32 they stay zero from the initial clear)
-  static constexpr int HN = wg_xr<S>() * 2 * PADMAX * NCH;
-  static constexpr int HPER = (HN + NT - 1) / NT;                // 2
+  static constexpr int HN = XR * 2 * PAD * NCH;
+  static constexpr int HPER = (HN + NT - 1) / NT;
   u32x4 x[XPER], d[DPER], hx[HPER];
   int xvalid;                                              // bit j: X chunk j inside the frame
   int hvalid;                                              // bit j: halo chunk j inside the frame
@@ -1270,7 +1302,7 @@ struct WBand {
       const int idx = tid + j * NT;
       const int q = idx % NCH, pc = idx / NCH;
       const int col = pc % IMG, row = pc / IMG;
-      const int iy = y0 + row - PADMAX;
+      const int iy = y0 + row - PAD;
       const int dy = iy < 0 ? -1 : (iy >= IMG ? 1 : 0);
       const bool ok = L.ty + dy >= 0 && L.ty + dy < nty;
       const int cy = ok ? iy - dy * IMG : 0;
@@ -1283,9 +1315,9 @@ struct WBand {
       for (int j = 0; j < HPER; ++j) {
         const int idx = tid + j * NT;
         const int q = idx % NCH, pc = idx / NCH;
-        const int k = pc % (2 * PADMAX), row = pc / (2 * PADMAX);
-        const int ix = k < PADMAX ? k - PADMAX : IMG + k - PADMAX;
-        const int iy = y0 + row - PADMAX;
+        const int k = pc % (2 * PAD), row = pc / (2 * PAD);
+        const int ix = k < PAD ? k - PAD : IMG + k - PAD;
+        const int iy = y0 + row - PAD;
         const int dy = iy < 0 ? -1 : (iy >= IMG ? 1 : 0), dx = ix < 0 ? -1 : 1;
         const bool ok = idx < HN && L.ty + dy >= 0 && L.ty + dy < nty && L.tx + dx >= 0 &&
                         L.tx + dx < ntx;
@@ -1309,17 +1341,17 @@ struct WBand {
       const int q = idx % NCH, pc = idx / NCH;
       const int col = pc % IMG, row = pc / IMG;
       const u32x4 z = {0u, 0u, 0u, 0u};
-      *(u32x4*)(xt + wx_off(row, col + PADMAX, q * CPB)) = (xvalid >> j) & 1 ? x[j] : z;
+      *(u32x4*)(xt + wx_off<PAD>(row, col + PAD, q * CPB)) = (xvalid >> j) & 1 ? x[j] : z;
     }
     if (tiled) {
 #pragma unroll
       for (int j = 0; j < HPER; ++j) {
         const int idx = tid + j * NT;
         const int q = idx % NCH, pc = idx / NCH;
-        const int k = pc % (2 * PADMAX), row = pc / (2 * PADMAX);
-        const int col = k < PADMAX ? k : IMG + k;
+        const int k = pc % (2 * PAD), row = pc / (2 * PAD);
+        const int col = k < PAD ? k : IMG + k;
         const u32x4 z = {0u, 0u, 0u, 0u};
-        if (idx < HN) *(u32x4*)(xt + wx_off(row, col, q * CPB)) = (hvalid >> j) & 1 ? hx[j] : z;
+        if (idx < HN) *(u32x4*)(xt + wx_off<PAD>(row, col, q * CPB)) = (hvalid >> j) & 1 ? hx[j] : z;
       }
     }
 #pragma unroll
@@ -1331,69 +1363,39 @@ struct WBand {
   }
 };
 
-// MFMAs of one band (this wave's taps {wave + 4m}).
-template <class S, int K>
-__device__ __forceinline__ void wgrad_band(f32x16 (&acc)[WG_NACC], const S* xt, const S* dt,
+// f32: MFMAs of one band for this wave's taps (element offsets toff).
+template <int K, int PAD>
+__device__ __forceinline__ void wgrad_band(f32x16 (&acc)[WG_NACC], const float* xt, const float* dt,
                                            const int (&toff)[WG_NACC], int lane) {
-  constexpr int off = PADMAX - K / 2;
-  if constexpr (sizeof(S) == 4) {
-    // k-step = 2 pixels (x0 + h); lane&31 is ci for A, n for B
-    const int ch = lane & 31, h = lane >> 5;
-    for (int yd = 0; yd < wg_rb<S>(); ++yd) {
-      const int xb = wx_off(yd + off, h + off, ch), db = wd_off(yd, h, ch);
-      for (int x0 = 0; x0 < IMG; x0 += 2) {
-        const float bv = dt[db + x0 * C];
+  constexpr int NACC = wg_nacc<PAD>();
+  constexpr int off = PAD - K / 2;
+  // k-step = 2 pixels (x0 + h); lane&31 is ci for A, n for B
+  const int ch = lane & 31, h = lane >> 5;
+  for (int yd = 0; yd < wg_rb<float, PAD>(); ++yd) {
+    const int xb = wx_off<PAD>(yd + off, h + off, ch), db = wd_off(yd, h, ch);
+    for (int x0 = 0; x0 < IMG; x0 += 2) {
+      const float bv = dt[db + x0 * C];
 #pragma unroll
-        for (int m = 0; m < WG_NACC; ++m) acc[m] = Tr<float>::mma(xt[xb + x0 * C + toff[m]], bv, acc[m]);
-      }
-    }
-  } else {
-    // k-step = 16 pixels.  Lane 4q+p' of each 16-lane group addresses pixel
-    // (x0 + 8 hh + q [+4]) and channels 16 (grp&1) + 4p' .. +3.  The 13 A
-    // fragments of the next k-step are read while this step's MFMAs run.
-    const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
-    const int chb = 16 * (grp & 1) + 4 * pp;
-    const int hh = grp >> 1;
-    constexpr int NSTEP = wg_rb<S>() * (IMG / 16);
-    auto xaddr = [&](int st) {
-      const int yd = st >> 1, dc0 = (st & 1) * 16 + 8 * hh + q;
-      return (const bf16_t*)xt + wx_off(yd + off, dc0 + off, chb);
-    };
-    auto daddr = [&](int st) {
-      const int yd = st >> 1, dc0 = (st & 1) * 16 + 8 * hh + q;
-      return (const bf16_t*)dt + wd_off(yd, dc0, chb);
-    };
-    bf16x8 av[2][WG_NACC], bv[2];
-    bv[0] = tr_read8(daddr(0));
-#pragma unroll
-    for (int m = 0; m < WG_NACC; ++m) av[0][m] = tr_read8(xaddr(0) + toff[m]);
-#pragma unroll
-    for (int st = 0; st < NSTEP; ++st) {
-      const int cur = st & 1, nxt = cur ^ 1;
-      if (st + 1 < NSTEP) {
-        bv[nxt] = tr_read8(daddr(st + 1));
-#pragma unroll
-        for (int m = 0; m < WG_NACC; ++m) av[nxt][m] = tr_read8(xaddr(st + 1) + toff[m]);
-      }
-#pragma unroll
-      for (int m = 0; m < WG_NACC; ++m) acc[m] = Tr<bf16_t>::mma(av[cur][m], bv[cur], acc[m]);
+      for (int m = 0; m < NACC; ++m) acc[m] = Tr<float>::mma(xt[xb + x0 * C + toff[m]], bv, acc[m]);
     }
   }
 }
 
-// bf16: tap-column blocking.  Wave w owns kernel columns kw0 = 2w, 2w + 1 (all
-// kh; 14 accumulator tiles, wave 3 only column 6 at K = 7).  The band's 16 B
-// fragments (8 D rows x 2 pixel blocks) are read once into registers; then for
-// every X row r of the band ONE A fragment per column feeds the MFMAs of all
-// taps kh with D row r - kh.  LDS reads per MFMA: 1/7 for A (was 1 with one
-// tap per A read) -- the old tap-scattered assignment was bound by the
-// transposing LDS reads.
-constexpr int WG2_NACC = 14;             // acc[j * 7 + kh]: tap (kh, kw0 + j)
-template <int K, int NKW>
+// bf16: tap-column blocking.  Wave w owns kernel columns kw0 = kwb + 2w, +1
+// and the kernel rows kh0 .. kh0+6 (< K) of its group (14 accumulator tiles).
+// The band's 16 B fragments (RB D rows x 2 pixel blocks) are read once into
+// registers; then for every X row r of the band ONE A fragment per column
+// feeds the MFMAs of all taps kh with D row r - kh.  LDS reads per MFMA: 1/7
+// for A (was 1 with one tap per A read) -- the old tap-scattered assignment
+// was bound by the transposing LDS reads.
+constexpr int WG2_NACC = 14;             // acc[j * 7 + kh - kh0]: tap (kh, kw0 + j)
+template <int K, int NKW, int PAD>
 __device__ __forceinline__ void wgrad_band2(f32x16 (&acc)[WG2_NACC], const bf16_t* xt,
-                                            const bf16_t* dt, int kw0, int lane) {
-  constexpr int off = PADMAX - K / 2;
-  constexpr int RB = wg_rb<bf16_t>();
+                                           const bf16_t* dt, int kw0, int kh0, int lane) {
+  constexpr int off = PAD - K / 2;
+  constexpr int RB = wg_rb<bf16_t, PAD>();
+  constexpr int NKH = K < 7 ? K : 7;               // kernel rows per group
+  const int nkh = K - kh0 < NKH ? K - kh0 : NKH;   // valid in this group (uniform)
   const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
   const int chb = 16 * (grp & 1) + 4 * pp;
   const int hh = grp >> 1;
@@ -1405,25 +1407,27 @@ __device__ __forceinline__ void wgrad_band2(f32x16 (&acc)[WG2_NACC], const bf16_
   // steps st = (X row r, pixel block): A fragments read one step ahead; the
   // sched_barriers keep the compiler from hoisting every read of the unrolled
   // band to the top (which spilled)
-  constexpr int NST = (RB + K - 1) * 2;
+  constexpr int NST = (RB + NKH - 1) * 2;
+  const int nst = (RB + nkh - 1) * 2;              // X rows this group's taps touch
   auto xaddr = [&](int st) {
-    return xt + wx_off((st >> 1) + off, (st & 1) * 16 + 8 * hh + q + off + kw0, chb);
+    return xt + wx_off<PAD>((st >> 1) + off + kh0, (st & 1) * 16 + 8 * hh + q + off + kw0, chb);
   };
   bf16x8 a0[2], a1[2];
   a0[0] = tr_read8(xaddr(0));
   if constexpr (NKW > 1) a1[0] = tr_read8(xaddr(0) + C);
 #pragma unroll
   for (int st = 0; st < NST; ++st) {
+    if (st >= nst) break;
     const int r = st >> 1, blk = st & 1, cur = st & 1, nxt = cur ^ 1;
-    if (st + 1 < NST) {
+    if (st + 1 < nst) {
       a0[nxt] = tr_read8(xaddr(st + 1));
       if constexpr (NKW > 1) a1[nxt] = tr_read8(xaddr(st + 1) + C);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int kh = 0; kh < K; ++kh) {
+    for (int kh = 0; kh < NKH; ++kh) {
       const int yd = r - kh;
-      if (yd >= 0 && yd < RB) {
+      if (yd >= 0 && yd < RB && kh < nkh) {
         acc[kh] = Tr<bf16_t>::mma(a0[cur], bv[yd][blk], acc[kh]);
         if constexpr (NKW > 1) acc[7 + kh] = Tr<bf16_t>::mma(a1[cur], bv[yd][blk], acc[7 + kh]);
       }
@@ -1432,35 +1436,47 @@ __device__ __forceinline__ void wgrad_band2(f32x16 (&acc)[WG2_NACC], const bf16_
   }
 }
 
-template <class S, int K, class Body>
+template <class S, int PAD, class Body>
 __device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
                                           const S* __restrict__ Ds, int B, int T, int g, int nwg,
                                           S* buf, int tid, int ablate, int ntx, int nty) {
   const bool tiled = ntx * nty > 1;
-  constexpr int BE = wgrad_band_elems<S>();
-  constexpr int NB = IMG / wg_rb<S>();                          // bands per (frame, clip)
+  constexpr int BE = wgrad_band_elems<S, PAD>();
+  constexpr int NBUF = wg_nbuf<S, PAD>();
+  constexpr int RB = wg_rb<S, PAD>();
+  constexpr int XE = wg_xr<S, PAD>() * tile_w<PAD>() * C;
+  constexpr int NB = IMG / RB;                                  // bands per (frame, clip)
   const int npairs = (B * T - g + nwg - 1) / nwg;
   const int nunits = npairs * NB;
-  // clear both buffers once (the X halo columns stay zero)
-  for (int i = tid; i < 2 * BE * (int)sizeof(S) / 16; i += NT)
+  // clear the buffers once (the X halo columns stay zero)
+  for (int i = tid; i < NBUF * BE * (int)sizeof(S) / 16; i += NT)
     ((u32x4*)buf)[i] = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
-  WBand<S> band;
+  WBand<S, PAD> band;
   if (nunits > 0) {
     band.load(Xs, Ds, B, g, 0, tid, ntx, nty);
-    band.store(buf, buf + wg_xr<S>() * TILE * C, tid, tiled);
+    band.store(buf, buf + XE, tid, tiled);
   }
   __syncthreads();
   for (int u = 0; u < nunits; ++u) {
-    S* xt = buf + (u & 1) * BE;
-    S* dt = xt + wg_xr<S>() * TILE * C;
+    S* xt = buf + (NBUF == 2 ? (u & 1) * BE : 0);
+    S* dt = xt + XE;
     const bool more = u + 1 < nunits;
-    if (more && !(ablate & 128))
-      band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * wg_rb<S>(), tid, ntx, nty);
+    // two buffers: the next band's loads are in flight under this band's MFMAs;
+    // one buffer (f32, PAD 7): load it after (the staged band would not fit
+    // in registers beside the accumulators)
+    if constexpr (NBUF == 2)
+      if (more && !(ablate & 128))
+        band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * RB, tid, ntx, nty);
     if (!(ablate & 64)) body(xt, dt);
     if (more) {
-      S* xn = buf + ((u + 1) & 1) * BE;
-      if (!(ablate & 128)) band.store(xn, xn + wg_xr<S>() * TILE * C, tid, tiled);
+      S* xn = buf + (NBUF == 2 ? ((u + 1) & 1) * BE : 0);
+      if constexpr (NBUF == 1) {
+        __syncthreads();                              // every wave is done reading the buffer
+        if (!(ablate & 128))
+          band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * RB, tid, ntx, nty);
+      }
+      if (!(ablate & 128)) band.store(xn, xn + XE, tid, tiled);
       __syncthreads();
     }
   }
@@ -1470,45 +1486,57 @@ __device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
 // k x k weight gradients over all (frame, clip) pairs:
 //   dW[n][ci][tap] = sum_{t,b,p} D_t[b][p][n] X_t[b][p + tap][ci]
 //   conv 0: (D, X) = (d ci_raw, gE)  -> w_inh;  conv 1: (d ce_raw, I_t) -> w_exc
-// Each wave owns taps {w, w+4, ...} (<= 13 32x32 accumulator tiles); the
-// D / X row bands are staged in LDS; per-workgroup partials go to wslab.
+// The D / X row bands are staged in LDS; per-workgroup partials go to wslab
+// [2][nwg][K*K][1024].  grid = (nwg, convs, tap groups).
 // =========================================================================
-template <class S>
+template <class S, int PAD>
 __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, int nwg, int conv0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   S* buf = (S*)smem;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = blockIdx.x, conv = blockIdx.y + conv0;
+  const int g = blockIdx.x, conv = blockIdx.y + conv0, grp = blockIdx.z;
   const int KK = a.K * a.K;
   const S* Xs = conv == 0 ? a.gE : a.I;
   const S* Ds = conv == 0 ? a.dci_s : a.dce_s;
 
-  float* dst = wslab + ((size_t)conv * nwg + g) * MAXTAP * 1024;
+  float* dst = wslab + ((size_t)conv * nwg + g) * KK * 1024;
   const int n = lane & 31;
   if constexpr (sizeof(S) == 2) {
     f32x16 acc[WG2_NACC];
 #pragma unroll
     for (int m = 0; m < WG2_NACC; ++m) acc[m] = zero16();
-    const int kw0 = 2 * wave;
+    const int nkwg = (a.K + 7) / 8;                  // column groups (1 for k <= 7)
+    const int kh0 = PAD == PADMAX ? 0 : (grp / nkwg) * 7;
+    const int kw0 = (PAD == PADMAX ? 0 : (grp % nkwg) * 8) + 2 * wave;
     auto run = [&](auto kc) {
       constexpr int K = decltype(kc)::value;
       // every wave runs two columns; a column kw >= K (wave 3's second at
       // K = 7) reads in-bounds LDS and its tiles are never stored: uniform
       // code, and that wave is otherwise idle while the others finish
-      wgrad_run<S, K>([&](const S* xt, const S* dt) { wgrad_band2<K, 2>(acc, xt, dt, kw0, lane); },
-                      Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
+      wgrad_run<S, PAD>(
+          [&](const S* xt, const S* dt) { wgrad_band2<K, 2, PAD>(acc, xt, dt, kw0, kh0, lane); },
+          Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
     };
-    switch (a.K) {
-      case 7: run(std::integral_constant<int, 7>{}); break;
-      case 5: run(std::integral_constant<int, 5>{}); break;
-      case 3: run(std::integral_constant<int, 3>{}); break;
-      default: run(std::integral_constant<int, 1>{}); break;
+    if constexpr (PAD == PADMAX) {
+      switch (a.K) {
+        case 7: run(std::integral_constant<int, 7>{}); break;
+        case 5: run(std::integral_constant<int, 5>{}); break;
+        case 3: run(std::integral_constant<int, 3>{}); break;
+        default: run(std::integral_constant<int, 1>{}); break;
+      }
+    } else {
+      switch (a.K) {
+        case 15: run(std::integral_constant<int, 15>{}); break;
+        case 13: run(std::integral_constant<int, 13>{}); break;
+        case 11: run(std::integral_constant<int, 11>{}); break;
+        default: run(std::integral_constant<int, 9>{}); break;
+      }
     }
-    // acc[j * 7 + kh]: rows ci = cl_x(r,h), cols n = lane&31
+    // acc[j * 7 + kh - kh0]: rows ci = cl_x(r,h), cols n = lane&31
 #pragma unroll
     for (int m = 0; m < WG2_NACC; ++m) {
-      const int kh = m % 7, kw = kw0 + m / 7;
+      const int kh = kh0 + m % 7, kw = kw0 + m / 7;
       if (kh < a.K && kw < a.K) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dst[(kh * a.K + kw) * 1024 + n * 32 + cl_x(r, h)] = acc[m][r];
@@ -1518,6 +1546,8 @@ __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, in
     f32x16 acc[WG_NACC];
 #pragma unroll
     for (int m = 0; m < WG_NACC; ++m) acc[m] = zero16();
+    constexpr int NACC = wg_nacc<PAD>();
+    const int tap0 = grp * 4 * NACC;
     // wave-uniform element offset of each tap; taps beyond K*K (the 13th slot
     // of waves 1-3 at K=7) read tap 0 and their accumulator is never stored,
     // so every MFMA is unconditional (no accumulator copies around branches)
@@ -1526,23 +1556,33 @@ __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, in
       int toff[WG_NACC];
 #pragma unroll
       for (int m = 0; m < WG_NACC; ++m) {
-        const int tap = wave + 4 * m < K * K ? wave + 4 * m : 0;
+        const int tap = m < NACC && tap0 + wave + 4 * m < K * K ? tap0 + wave + 4 * m : 0;
         const int kh = tap / K, kw = tap - kh * K;
-        toff[m] = (kh * TILE + kw) * C;
+        toff[m] = (kh * tile_w<PAD>() + kw) * C;
       }
-      wgrad_run<S, K>([&](const S* xt, const S* dt) { wgrad_band<S, K>(acc, xt, dt, toff, lane); },
-                      Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
+      wgrad_run<S, PAD>(
+          [&](const S* xt, const S* dt) { wgrad_band<K, PAD>(acc, (const float*)xt, (const float*)dt, toff, lane); },
+          Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
     };
-    switch (a.K) {
-      case 7: run(std::integral_constant<int, 7>{}); break;
-      case 5: run(std::integral_constant<int, 5>{}); break;
-      case 3: run(std::integral_constant<int, 3>{}); break;
-      default: run(std::integral_constant<int, 1>{}); break;
+    if constexpr (PAD == PADMAX) {
+      switch (a.K) {
+        case 7: run(std::integral_constant<int, 7>{}); break;
+        case 5: run(std::integral_constant<int, 5>{}); break;
+        case 3: run(std::integral_constant<int, 3>{}); break;
+        default: run(std::integral_constant<int, 1>{}); break;
+      }
+    } else {
+      switch (a.K) {
+        case 15: run(std::integral_constant<int, 15>{}); break;
+        case 13: run(std::integral_constant<int, 13>{}); break;
+        case 11: run(std::integral_constant<int, 11>{}); break;
+        default: run(std::integral_constant<int, 9>{}); break;
+      }
     }
     // acc[m]: rows ci = cl_x(r,h), cols n = lane&31
 #pragma unroll
-    for (int m = 0; m < WG_NACC; ++m) {
-      const int tap = wave + 4 * m;
+    for (int m = 0; m < NACC; ++m) {
+      const int tap = tap0 + wave + 4 * m;
       if (tap < KK) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dst[tap * 1024 + n * 32 + cl_x(r, h)] = acc[m][r];
@@ -1602,8 +1642,9 @@ __global__ void k_prep(PrepArgs<S> p) {
 // ---------------------------------------------------------------- reductions
 struct ReduceArgs {
   int B, K, nwg;
-  const float* slab;    // [B][SLAB]
-  const float* wslab;   // [2][nwg][49][1024]
+  int Cu;               // the caller's channel count (<= 32); padded channels are dropped
+  const float* slab;    // [rows][SLAB]
+  const float* wslab;   // [2][nwg][K*K][1024]
   pt_cell_grads g;
 };
 
@@ -1636,10 +1677,11 @@ __global__ void k_reduce(ReduceArgs r) {
     if (e < n_small) {
       const float s = strided_sum(r.slab + e, SLAB, r.B);
       if (e < SLAB_G) {
-        const int gate = e / 1024;
-        if (r.g.gate_w[gate]) r.g.gate_w[gate][e % 1024] = s;
+        const int gate = e / 1024, n = (e % 1024) / 32, ci = e % 32;
+        if (r.g.gate_w[gate] && n < r.Cu && ci < r.Cu) r.g.gate_w[gate][n * r.Cu + ci] = s;
       } else {
         const int slot = (e - SLAB_G) / 32, c = (e - SLAB_G) % 32;
+        if (c >= r.Cu) continue;
         switch (slot) {
           case SM_ALPHA: if (r.g.alpha) r.g.alpha[c] = s; break;
           case SM_MU: if (r.g.mu) r.g.mu[c] = s; break;
@@ -1672,38 +1714,120 @@ __global__ void k_reduce(ReduceArgs r) {
       const int e2 = e - n_small;
       const int conv = e2 / (KK * 1024), rem = e2 % (KK * 1024);
       const int tap = rem / 1024, nc = rem % 1024, n = nc / 32, ci = nc % 32;
-      const float s = strided_sum(r.wslab + ((size_t)conv * r.nwg * MAXTAP + tap) * 1024 + nc,
-                                  (size_t)MAXTAP * 1024, r.nwg);
+      const float s = strided_sum(r.wslab + ((size_t)conv * r.nwg * KK + tap) * 1024 + nc,
+                                  (size_t)KK * 1024, r.nwg);
       float* W = conv == 0 ? r.g.w_inh : r.g.w_exc;
-      if (W) W[(n * C + ci) * KK + tap] = s;
+      if (W && n < r.Cu && ci < r.Cu) W[(n * r.Cu + ci) * KK + tap] = s;
     }
   }
 }
 
-// channels-last tiles [B tiles][32][32][C] (S)  <->  NCHW fp32 frames
-__device__ __forceinline__ size_t nchw_off(int v, int pix, int c, int T, int t, int ntx, int nty) {
+// channels-last tiles [B tiles][32][32][C] (S)  <->  NCHW fp32 frames of the
+// caller's Cu <= 32 channels (the padded channels are dropped / zero)
+__device__ __forceinline__ size_t nchw_off(int v, int pix, int c, int T, int t, int ntx, int nty,
+                                           int Cu) {
   const TileLoc L = tile_loc(v, ntx, nty);
   const int W = ntx * IMG;
-  return (((size_t)L.b * T + t) * C + c) * ((size_t)nty * IMG * W) +
+  return (((size_t)L.b * T + t) * Cu + c) * ((size_t)nty * IMG * W) +
          (size_t)(L.ty * IMG + (pix >> 5)) * W + L.tx * IMG + (pix & 31);
 }
 template <class S>
 __global__ void k_to_nchw(const S* __restrict__ src, float* __restrict__ dst, int B, int T, int t,
-                          int ntx, int nty) {
-  // dst [clips][T][C][H][W] (T=1,t=0 for a single frame); B = tiles
+                          int ntx, int nty, int Cu) {
+  // dst [clips][T][Cu][H][W] (T=1,t=0 for a single frame); B = tiles
   const int n = B * NPIX * C;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int c = e % C, pix = (e / C) % NPIX, v = e / (C * NPIX);
-    dst[nchw_off(v, pix, c, T, t, ntx, nty)] = ldf(src + e);
+    if (c < Cu) dst[nchw_off(v, pix, c, T, t, ntx, nty, Cu)] = ldf(src + e);
   }
 }
 __global__ void k_from_nchw(const float* __restrict__ src, float* __restrict__ dst, int B, int ntx,
-                            int nty) {
+                            int nty, int Cu) {
   const int n = B * NPIX * C;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int c = e % C, pix = (e / C) % NPIX, v = e / (C * NPIX);
-    dst[e] = src[nchw_off(v, pix, c, 1, 0, ntx, nty)];
+    dst[e] = c < Cu ? src[nchw_off(v, pix, c, 1, 0, ntx, nty, Cu)] : 0.f;
   }
+}
+
+// Channel padding (Cu < 32): the caller's parameters copied into 32-channel
+// buffers, zero outside [0, Cu) (rows and columns of every weight, biases,
+// per-channel and BatchNorm parameters).  A padded channel receives no input
+// from a real one (zero weight columns) and sends none (zero weight rows), so
+// the real channels compute exactly the Cu-channel model; the padded ones
+// stay finite (BatchNorm of an all-zero conv output is 0) and their
+// gradients are dropped by k_reduce.  The padded tensors live in the saved
+// blob: the backward reads the same values.
+struct PadArgs {
+  int Cu, KK;
+  pt_cell_params src;   // caller layout ([Cu]..., [Cu][Cu][K][K], ...)
+  float* dst;           // packed 32-channel copies, layout of pad_layout()
+};
+struct PadLayout {      // float offsets into PadArgs::dst
+  size_t pw, pb, w_exc, w_inh, alpha, mu, gamma, kappa, gw[6], gb[6], bnw[2], bnb[2], total;
+};
+__host__ __device__ inline PadLayout pad_layout(int KK) {
+  PadLayout l{};
+  size_t o = 0;
+  l.pw = o; o += 32 * 3;
+  l.pb = o; o += 32;
+  l.w_exc = o; o += (size_t)32 * 32 * KK;
+  l.w_inh = o; o += (size_t)32 * 32 * KK;
+  l.alpha = o; o += 32; l.mu = o; o += 32; l.gamma = o; o += 32; l.kappa = o; o += 32;
+  for (int i = 0; i < 6; ++i) { l.gw[i] = o; o += 1024; }
+  for (int i = 0; i < 6; ++i) { l.gb[i] = o; o += 32; }
+  for (int i = 0; i < 2; ++i) { l.bnw[i] = o; o += 32; }
+  for (int i = 0; i < 2; ++i) { l.bnb[i] = o; o += 32; }
+  l.total = o;
+  return l;
+}
+__global__ void k_pad_params(PadArgs a) {
+  const PadLayout l = pad_layout(a.KK);
+  const int Cu = a.Cu, KK = a.KK;
+  auto vec = [&](const float* s, size_t off, size_t e) {       // [32] <- [Cu]
+    a.dst[off + e] = s && (int)e < Cu ? s[e] : 0.f;
+  };
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < l.total;
+       e += (size_t)gridDim.x * blockDim.x) {
+    if (e < l.pb) {                                    // preproc [32][3]
+      const int c = (int)(e / 3), k = (int)(e % 3);
+      a.dst[e] = c < Cu ? a.src.preproc_w[c * 3 + k] : 0.f;
+    } else if (e < l.w_exc) {
+      vec(a.src.preproc_b, l.pb, e - l.pb);
+    } else if (e < l.alpha) {                          // w_exc, w_inh [32][32][KK]
+      const bool inh = e >= l.w_inh;
+      const size_t r = e - (inh ? l.w_inh : l.w_exc);
+      const int n = (int)(r / (32 * KK)), ci = (int)(r / KK % 32), tap = (int)(r % KK);
+      const float* W = inh ? a.src.w_inh : a.src.w_exc;
+      a.dst[e] = W && n < Cu && ci < Cu ? W[((size_t)n * Cu + ci) * KK + tap] : 0.f;
+    } else if (e < l.gw[0]) {                          // alpha, mu, gamma, kappa
+      const int which = (int)((e - l.alpha) / 32);
+      const float* p4[4] = {a.src.alpha, a.src.mu, a.src.gamma, a.src.kappa};
+      vec(p4[which], l.alpha + which * 32, (e - l.alpha) % 32);
+    } else if (e < l.gb[0]) {                          // gate weights [32][32]
+      const int gi = (int)((e - l.gw[0]) / 1024), r = (int)((e - l.gw[0]) % 1024);
+      const int n = r / 32, ci = r % 32;
+      a.dst[e] = n < Cu && ci < Cu ? a.src.gate_w[gi][n * Cu + ci] : 0.f;
+    } else if (e < l.bnw[0]) {
+      const int gi = (int)((e - l.gb[0]) / 32);
+      vec(a.src.gate_b[gi], l.gb[gi], (e - l.gb[0]) % 32);
+    } else {                                           // bn weights / biases
+      const int k = (int)((e - l.bnw[0]) / 32);
+      const float* src = k < 2 ? a.src.bn_w[k] : a.src.bn_b[k - 2];
+      vec(src, l.bnw[0] + k * 32, (e - l.bnw[0]) % 32);
+    }
+  }
+}
+// pt_cell_params view of the padded copies
+inline pt_cell_params padded_params(const float* base, int KK, bool no_inh) {
+  const PadLayout l = pad_layout(KK);
+  pt_cell_params p{};
+  p.preproc_w = base + l.pw; p.preproc_b = base + l.pb;
+  p.w_exc = base + l.w_exc; p.w_inh = no_inh ? nullptr : base + l.w_inh;
+  p.alpha = base + l.alpha; p.mu = base + l.mu; p.gamma = base + l.gamma; p.kappa = base + l.kappa;
+  for (int i = 0; i < 6; ++i) { p.gate_w[i] = base + l.gw[i]; p.gate_b[i] = base + l.gb[i]; }
+  for (int i = 0; i < 2; ++i) { p.bn_w[i] = base + l.bnw[i]; p.bn_b[i] = base + l.bnb[i]; }
+  return p;
 }
 
 }  // namespace ptc
@@ -1762,11 +1886,12 @@ inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Plan {
   int B, T, K, dt;
+  int Cu;             // caller's channels (<= 32); < 32: padded parameter copies at o_pad
   int ntx, nty;       // tiles per frame; B counts tiles (clips * ntx * nty)
   size_t es;          // element size of S
   size_t frame;       // elements per frame tensor (B*NPIX*C)
   // saved offsets
-  size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], saved;
+  size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], o_pad, saved;
   // workspace offsets
   size_t o_bnacc, o_bnbacc, o_tr[NTRANS], o_dci, o_dce, o_slab, o_wslab, ws;
   int nwg;
@@ -1774,13 +1899,14 @@ struct Plan {
 
 int check(const pt_cell_desc* d) {
   if (!d) return fail(PT_ERR_ARG, "null descriptor%s%ld");
-  if (d->channels != 32) return fail(PT_ERR_UNSUPPORTED, "channels must be 32 (got %s%ld)", "", d->channels);
+  if (d->channels < 1 || d->channels > 32)
+    return fail(PT_ERR_UNSUPPORTED, "channels must be in [1, 32]%s (got %ld)", "", d->channels);
   if (d->height < 32 || d->height % 32 || d->height > 1024)
     return fail(PT_ERR_UNSUPPORTED, "height must be a multiple of 32 in [32, 1024]%s (got %ld)", "", d->height);
   if (d->width < 32 || d->width % 32 || d->width > 1024)
     return fail(PT_ERR_UNSUPPORTED, "width must be a multiple of 32 in [32, 1024]%s (got %ld)", "", d->width);
-  if (d->ksize < 1 || d->ksize > 7 || (d->ksize & 1) == 0)
-    return fail(PT_ERR_UNSUPPORTED, "ksize must be odd and <= 7%s (got %ld)", "", d->ksize);
+  if (d->ksize < 1 || d->ksize > 15 || (d->ksize & 1) == 0)
+    return fail(PT_ERR_UNSUPPORTED, "ksize must be odd and <= 15%s (got %ld)", "", d->ksize);
   if (d->batch < 1 || d->frames < 1) return fail(PT_ERR_ARG, "batch and frames must be >= 1%s%ld");
   if (d->act != PT_ACT_SOFTPLUS && d->act != PT_ACT_TANH) return fail(PT_ERR_ARG, "bad act%s%ld");
   if (d->dtype != PT_DTYPE_F32 && d->dtype != PT_DTYPE_BF16) return fail(PT_ERR_ARG, "bad dtype%s%ld");
@@ -1807,8 +1933,10 @@ Plan plan(const pt_cell_desc* d) {
   p.o_eg = o; o += fbytes;
   p.o_at = o; o += d->cell == PT_CELL_HGRU ? fbytes : 0;
   p.o_bnstat = o; o += al((size_t)p.T * 128 * 4);
-  for (int i = 0; i < 4; ++i) { p.o_wf[i] = o; o += al((size_t)C * C * MAXTAP * p.es); }
+  for (int i = 0; i < 4; ++i) { p.o_wf[i] = o; o += al((size_t)C * C * p.K * p.K * p.es); }
   for (int i = 0; i < 12; ++i) { p.o_g[i] = o; o += al((size_t)C * C * p.es); }
+  p.Cu = d->channels;
+  p.o_pad = o; o += p.Cu < C ? al(pad_layout(p.K * p.K).total * 4) : 0;
   p.saved = o;
   o = 0;
   p.o_bnacc = o; o += al((size_t)p.T * 2 * NBNC * 96 * 8);
@@ -1818,7 +1946,7 @@ Plan plan(const pt_cell_desc* d) {
   p.o_dce = o; o += fbytes;
   p.o_slab = o; o += al((size_t)p.B * PW_PARTS * SLAB * 4);
   p.nwg = p.B * p.T < 256 ? p.B * p.T : 256;
-  p.o_wslab = o; o += al((size_t)2 * p.nwg * MAXTAP * 1024 * 4);
+  p.o_wslab = o; o += al((size_t)2 * p.nwg * p.K * p.K * 1024 * 4);
   p.ws = o;
   return p;
 }
@@ -1829,6 +1957,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   using F = typename Tr<S>::frag;
   memset(&a, 0, sizeof(a));
   a.B = p.B; a.T = p.T; a.K = p.K; a.act = d->act; a.no_inh = d->no_inh; a.eps = d->eps;
+  a.Cu = p.Cu;
   a.ntx = p.ntx; a.nty = p.nty;
   a.hgru = d->cell == PT_CELL_HGRU;
   a.x = x;
@@ -1889,8 +2018,10 @@ template <class S>
 int set_lds_attrs() {
   static thread_local bool done = false;   // per host thread; cheap either way
   if (done) return 0;
-  SETLDS((k_conv_fwd<S>), conv_lds_bytes<S>());
-  SETLDS((k_conv_bwd<S>), conv_lds_bytes<S>());
+  SETLDS((k_conv_fwd<S, PADMAX>), (conv_lds_bytes<S, PADMAX>()));
+  SETLDS((k_conv_bwd<S, PADMAX>), (conv_lds_bytes<S, PADMAX>()));
+  SETLDS((k_conv_fwd<S, PADBIG>), (conv_lds_bytes<S, PADBIG>()));
+  SETLDS((k_conv_bwd<S, PADBIG>), (conv_lds_bytes<S, PADBIG>()));
   SETLDS((k_bnbwd_fill<S>), conv_lds_bytes<S>());
   SETLDS((k_pw_fa<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
@@ -1908,9 +2039,26 @@ int set_lds_attrs() {
   SETLDS((k_pw_fb<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
   SETLDS((k_pw_bb<S, 1, 1>), (pwb_lds_bytes<S>()));
-  SETLDS(k_wgrad<S>, wgrad_lds_bytes<S>());
+  SETLDS((k_wgrad<S, PADMAX>), (wgrad_lds_bytes<S, PADMAX>()));
+  SETLDS((k_wgrad<S, PADBIG>), (wgrad_lds_bytes<S, PADBIG>()));
   done = true;
   return 0;
+}
+
+// conv launches: the 38 x 38-tile kernels for k <= 7, the 46 x 46 ones above
+template <class S>
+void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
+  if (p.K <= 2 * PADMAX + 1)
+    hipLaunchKernelGGL((k_conv_fwd<S, PADMAX>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADMAX>()), st, c);
+  else
+    hipLaunchKernelGGL((k_conv_fwd<S, PADBIG>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADBIG>()), st, c);
+}
+template <class S>
+void launch_conv_bwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
+  if (p.K <= 2 * PADMAX + 1)
+    hipLaunchKernelGGL((k_conv_bwd<S, PADMAX>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADMAX>()), st, c);
+  else
+    hipLaunchKernelGGL((k_conv_bwd<S, PADBIG>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADBIG>()), st, c);
 }
 
 template <class S>
@@ -1927,6 +2075,13 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
                 void* ws, float* e_last, float* gates, hipStream_t st) {
   const Plan p = plan(d);
   if (int rc = set_lds_attrs<S>()) return rc;
+  pt_cell_params padded;
+  if (p.Cu < C) {            // fewer channels than the MFMA tile: zero-padded copies (k_pad_params)
+    PadArgs pad{p.Cu, p.K * p.K, *pr, (float*)((char*)saved + p.o_pad)};
+    hipLaunchKernelGGL(k_pad_params, dim3(256), dim3(256), 0, st, pad);
+    padded = padded_params(pad.dst, p.K * p.K, d->no_inh);
+    pr = &padded;
+  }
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
   a.gates = gates;
@@ -1942,7 +2097,7 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   HIPCHK(zero_async((char*)ws + p.o_bnacc, (size_t)p.T * 2 * NBNC * 96 * 8, st));
   timed(PT_K_PREP, st, [&] { hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa); });
   const dim3 gpf(p.B * PWF_WGPC);
-  const size_t lpf = (pw_lds_bytes<PWF_RPP, false>()), lcv = conv_lds_bytes<S>();
+  const size_t lpf = (pw_lds_bytes<PWF_RPP, false>());
   const size_t fs = p.frame;
   ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
   ca.wf = a.wf_inh;
@@ -1954,16 +2109,17 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
     if (!d->no_inh) {
       ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96;
       timed(PT_K_CONV_FA, st, [&] {
-        hipLaunchKernelGGL((k_conv_fwd<S>), dim3(p.B), dim3(NT), lcv, st, ca); });
+        launch_conv_fwd<S>(p, st, ca); });
     }
     timed(PT_K_PW_FB, st, [&] { PW_LAUNCH(k_pw_fb, gpf, lpf); });
     cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * NBNC * 96;
     timed(PT_K_CONV_FB, st, [&] {
-      hipLaunchKernelGGL((k_conv_fwd<S>), dim3(p.B), dim3(NT), lcv, st, cb); });
+      launch_conv_fwd<S>(p, st, cb); });
   }
   if (e_last)
     hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, st,
-                       (const float*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0, p.ntx, p.nty);
+                       (const float*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0, p.ntx, p.nty,
+                       p.Cu);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1974,12 +2130,17 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
                  hipStream_t st) {
   const Plan p = plan(d);
   if (int rc = set_lds_attrs<S>()) return rc;
+  pt_cell_params padded;
+  if (p.Cu < C) {            // the forward's padded copies
+    padded = padded_params((const float*)((const char*)saved + p.o_pad), p.K * p.K, d->no_inh);
+    pr = &padded;
+  }
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
   HIPCHK(zero_async((char*)ws + p.o_slab, (size_t)p.B * PW_PARTS * SLAB * 4, st));
   HIPCHK(zero_async((char*)ws + p.o_bnbacc, (size_t)p.T * 2 * NBNC * 64 * 8, st));
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
-                     (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty);
+                     (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty, p.Cu);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
   const size_t lpa = (pw_lds_bytes<PWA_RPP, true>()), lpb = pwb_lds_bytes<S>();
   const size_t lcv = conv_lds_bytes<S>();
@@ -1995,7 +2156,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
     cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
     cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
     timed(PT_K_CONV_BB, st, [&] {
-      hipLaunchKernelGGL((k_conv_bwd<S>), dim3(p.B), dim3(NT), lcv, st, cb); });
+      launch_conv_bwd<S>(p, st, cb); });
     a.t = t;
     timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
     a.conv_done = 0;
@@ -2007,7 +2168,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
       if (t >= 1) {
         timed(PT_K_CONV_BA, st, [&] {
-          hipLaunchKernelGGL((k_conv_bwd<S>), dim3(p.B), dim3(NT), lcv, st, ca); });
+          launch_conv_bwd<S>(p, st, ca); });
         a.conv_done = 1;
       } else {
         timed(PT_K_CONV_BA, st, [&] {
@@ -2019,15 +2180,21 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   }
   float* wslab = (float*)((char*)ws + p.o_wslab);
   const int conv0 = d->no_inh ? 1 : 0;
-  if (d->no_inh) HIPCHK(zero_async(wslab, (size_t)p.nwg * MAXTAP * 1024 * 4, st));
+  if (d->no_inh) HIPCHK(zero_async(wslab, (size_t)p.nwg * p.K * p.K * 1024 * 4, st));
   timed(PT_K_WGRAD, st, [&] {
-    hipLaunchKernelGGL(k_wgrad<S>, dim3(p.nwg, 2 - conv0), dim3(NT), wgrad_lds_bytes<S>(), st, a,
-                       wslab, p.nwg, conv0); });
+    const dim3 grid(p.nwg, 2 - conv0, wgrad_groups(p.K, sizeof(S) == 2));
+    if (p.K <= 2 * PADMAX + 1)
+      hipLaunchKernelGGL((k_wgrad<S, PADMAX>), grid, dim3(NT), (wgrad_lds_bytes<S, PADMAX>()), st, a,
+                         wslab, p.nwg, conv0);
+    else
+      hipLaunchKernelGGL((k_wgrad<S, PADBIG>), grid, dim3(NT), (wgrad_lds_bytes<S, PADBIG>()), st, a,
+                         wslab, p.nwg, conv0); });
   ReduceArgs r;
   r.B = p.B * PW_PARTS; r.K = p.K; r.nwg = p.nwg;
   r.slab = (const float*)((char*)ws + p.o_slab);
   r.wslab = wslab;
   r.g = *g;
+  r.Cu = p.Cu;
   if (d->no_inh) { r.g.w_inh = nullptr; r.g.alpha = nullptr; r.g.mu = nullptr;
                    r.g.bn_w[0] = nullptr; r.g.bn_b[0] = nullptr;
                    r.g.gate_w[2] = r.g.gate_w[3] = nullptr; r.g.gate_b[2] = r.g.gate_b[3] = nullptr; }
@@ -2086,7 +2253,7 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, p
   for (int t = 0; t < p.T; ++t) {
     hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, (hipStream_t)stream,   // E is f32
                        (const float*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B,
-                       p.T, t, p.ntx, p.nty);
+                       p.T, t, p.ntx, p.nty, p.Cu);
   }
   HIPCHK(hipGetLastError());
   return 0;

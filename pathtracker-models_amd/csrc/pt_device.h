@@ -27,12 +27,15 @@ namespace ptc {
 constexpr int C = 32;          // channels (MFMA tile width)
 constexpr int IMG = 32;        // H = W = 32
 constexpr int NPIX = IMG * IMG;
-constexpr int PADMAX = 3;      // halo for k <= 7
+constexpr int PADMAX = 3;      // halo for k <= 7 (the engine's k = 7: the fast path)
 constexpr int TILE = IMG + 2 * PADMAX;   // 38
+constexpr int PADBIG = 7;      // halo for 9 <= k <= 15 (the reference constructors' default k = 15)
+template <int PAD> constexpr int tile_w() { return IMG + 2 * PAD; }   // 38 / 46
+constexpr int pad_for(int K) { return K <= 2 * PADMAX + 1 ? PADMAX : PADBIG; }
 constexpr int NT = 256;        // threads per block
 constexpr int NWAVE = NT / 64;
 constexpr int RPW = IMG / NWAVE;         // image rows per wave (8)
-constexpr int MAXTAP = 49;
+constexpr int MAXTAP = 49;     // taps at PAD = PADMAX (k <= 7)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -348,22 +351,22 @@ __device__ __forceinline__ f32x16 wgrad_cl(const f32x16& d, const V& x, f32x16 a
 // [TILE rows][TILE cols][CP channels] of S, zero halo.  bf16: 16-B chunks of
 // 8 channels XOR-swizzled by (col >> 2) & 3 so the 32 lanes of an A-fragment
 // read (consecutive columns, same chunk) hit distinct bank groups.
-template <class S> __device__ __forceinline__ int tile_off(int trow, int tcol, int ch);
-template <> __device__ __forceinline__ int tile_off<float>(int trow, int tcol, int ch) {
-  return (trow * TILE + tcol) * Tr<float>::CP + ch;
+// PAD = halo width: PADMAX (38 x 38 tile) for k <= 7, PADBIG (46 x 46) above.
+template <class S, int PAD = PADMAX>
+__device__ __forceinline__ int tile_off(int trow, int tcol, int ch) {
+  constexpr int TW = tile_w<PAD>();
+  if constexpr (sizeof(S) == 4) return (trow * TW + tcol) * Tr<float>::CP + ch;
+  else return (trow * TW + tcol) * 32 + ((((ch >> 3) ^ ((tcol >> 2) & 3))) << 3) + (ch & 7);
 }
-template <> __device__ __forceinline__ int tile_off<bf16_t>(int trow, int tcol, int ch) {
-  return (trow * TILE + tcol) * 32 + ((((ch >> 3) ^ ((tcol >> 2) & 3))) << 3) + (ch & 7);
-}
-template <class S>
+template <class S, int PAD = PADMAX>
 __host__ __device__ constexpr int tile_bytes() {
-  return TILE * TILE * Tr<S>::CP * (int)sizeof(S);
+  return tile_w<PAD>() * tile_w<PAD>() * Tr<S>::CP * (int)sizeof(S);
 }
 
-template <class S>
+template <class S, int PAD = PADMAX>
 __device__ void tile_zero(S* tile, int tid) {
   uint4* p = (uint4*)tile;
-  const int n = tile_bytes<S>() / 16;
+  const int n = tile_bytes<S, PAD>() / 16;
   for (int i = tid; i < n; i += NT) p[i] = make_uint4(0, 0, 0, 0);
 }
 
@@ -371,7 +374,7 @@ __device__ void tile_zero(S* tile, int tid) {
 // channels-last clip image (global, [32][32][32] of S).  All 16 loads of a
 // thread are issued before any LDS store so one memory round trip covers the
 // whole 64 KB image (one wave per SIMD has nothing else to hide latency with).
-template <class S>
+template <class S, int PAD = PADMAX>
 __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restrict__ src,
                                           int pass, int tid) {
   constexpr int CPB = 16 / (int)sizeof(S);          // channels per 16-B chunk
@@ -389,7 +392,7 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
     const int idx = tid + k * NT;
     const int pix = idx / NCH, q = idx % NCH;
     const int y = pix >> 5, x = pix & 31;
-    *(uint4*)(tile + tile_off<S>(y + PADMAX, x + PADMAX, q * CPB)) = v[k];
+    *(uint4*)(tile + tile_off<S, PAD>(y + PAD, x + PAD, q * CPB)) = v[k];
   }
 }
 
@@ -459,33 +462,45 @@ struct NoRowHook {
   static constexpr bool active = false;
 };
 
-template <class S, int K, class Fill, class Done = NoRowHook>
+// k > 7 (PAD = PADBIG): the 46 x 46 tile leaves no LDS for weight slices;
+// every wave reads its column's K x KSP B fragments straight from L2 at the
+// top of the column (the ~K * RPW * KSP MFMAs of the column cover the fetch).
+template <class S, int K, int PAD, class Fill, class Done = NoRowHook>
 __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
                                            const typename Tr<S>::frag* __restrict__ wf, S* tile,
                                            char* wbuf, int row0, int lane, int tid, int ablate,
                                            const Done& done = Done()) {
   using TT = Tr<S>;
   using F = typename TT::frag;
+  constexpr bool LDSW = K <= 2 * PADMAX + 1;  // weight slices staged in LDS
   constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
-  constexpr int off = PADMAX - K / 2;
+  constexpr int off = PAD - K / 2;
   constexpr int NTR = RPW + K - 1;          // tile rows touched by this wave
   const int h = lane >> 5, px = lane & 31;
   for (int pass = 0; pass < TT::NPASS; ++pass) {
     WSlice pre;
-    wslice_load<S, K>(pre, wf, pass, 0, tid);
+    if constexpr (LDSW) wslice_load<S, K>(pre, wf, pass, 0, tid);
     __syncthreads();
     if (!(ablate & 2)) fill(pass);
-    wslice_store<K>(pre, wbuf, tid);
+    if constexpr (LDSW) wslice_store<K>(pre, wbuf, tid);
     __syncthreads();
     if (ablate & 1) continue;
     for (int kw = 0; kw < K; ++kw) {
-      const F* wl = (const F*)(wbuf + (kw & 1) * WSLICE_BYTES) + lane;
-      if (kw + 1 < K) wslice_load<S, K>(pre, wf, pass, kw + 1, tid);
       F bc[K][KSP];
+      if constexpr (LDSW) {
+        const F* wl = (const F*)(wbuf + (kw & 1) * WSLICE_BYTES) + lane;
+        if (kw + 1 < K) wslice_load<S, K>(pre, wf, pass, kw + 1, tid);
 #pragma unroll
-      for (int kh = 0; kh < K; ++kh)
+        for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-        for (int s = 0; s < KSP; ++s) bc[kh][s] = wl[(kh * KSP + s) * 64];
+          for (int s = 0; s < KSP; ++s) bc[kh][s] = wl[(kh * KSP + s) * 64];
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+          for (int s = 0; s < KSP; ++s)
+            bc[kh][s] = wf[((kh * K + kw) * TT::KS + pass * KSP + s) * 64 + lane];
+      }
       const int tcol = px + kw + off;
       // A fragments of tile row tr, software-pipelined CONV_PF rows ahead of
       // their MFMAs (one wave per SIMD: nothing else hides LDS latency)
@@ -495,9 +510,9 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
 #pragma unroll
         for (int s = 0; s < KSP; ++s) {
           if constexpr (sizeof(S) == 4) {
-            av[tr][s] = tile[tile_off<S>(trow, tcol, 2 * s + h)];
+            av[tr][s] = tile[tile_off<S, PAD>(trow, tcol, 2 * s + h)];
           } else {
-            av[tr][s] = *(const bf16x8*)(tile + tile_off<S>(trow, tcol, 16 * s + 8 * h));
+            av[tr][s] = *(const bf16x8*)(tile + tile_off<S, PAD>(trow, tcol, 16 * s + 8 * h));
           }
         }
       };
@@ -523,24 +538,35 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
           if (i >= 0 && i < RPW && kw == K - 1 && pass == TT::NPASS - 1) done(i, acc[i < 0 ? 0 : i]);
         }
       }
-      if (kw + 1 < K) {
-        wslice_store<K>(pre, wbuf + ((kw + 1) & 1) * WSLICE_BYTES, tid);
-        __syncthreads();
+      if constexpr (LDSW) {
+        if (kw + 1 < K) {
+          wslice_store<K>(pre, wbuf + ((kw + 1) & 1) * WSLICE_BYTES, tid);
+          __syncthreads();
+        }
       }
     }
   }
 }
 
-template <class S, class Fill, class Done = NoRowHook>
+template <class S, int PAD, class Fill, class Done = NoRowHook>
 __device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], Fill& fill,
                                          const typename Tr<S>::frag* __restrict__ wf, S* tile,
                                          char* wbuf, int K, int row0, int lane, int tid,
                                          int ablate, const Done& done = Done()) {
-  switch (K) {
-    case 7: conv_run_k<S, 7>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-    case 5: conv_run_k<S, 5>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-    case 3: conv_run_k<S, 3>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-    default: conv_run_k<S, 1>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+  if constexpr (PAD == PADMAX) {
+    switch (K) {
+      case 7: conv_run_k<S, 7, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 5: conv_run_k<S, 5, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 3: conv_run_k<S, 3, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      default: conv_run_k<S, 1, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+    }
+  } else {
+    switch (K) {
+      case 15: conv_run_k<S, 15, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 13: conv_run_k<S, 13, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 11: conv_run_k<S, 11, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      default: conv_run_k<S, 9, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+    }
   }
 }
 

@@ -106,10 +106,10 @@ def run_recurrent(model, x, y, want_gates):
 
 
 def make_int(ref_int, tag, *, batch, t_len, dims, act="softplus", no_inh=False,
-             lesion=(), want_gates=True, seed=0, hw=(32, 32)):
+             lesion=(), want_gates=True, seed=0, hw=(32, 32), k=7):
     synth = _synth()
     torch.manual_seed(1000 + seed)
-    kw = dict(dimensions=dims, timesteps=t_len, kernel_size=7, jacobian_penalty=False,
+    kw = dict(dimensions=dims, timesteps=t_len, kernel_size=k, jacobian_penalty=False,
               grad_method="bptt", no_inh=no_inh)
     for les in lesion:
         kw["lesion_" + les] = True
@@ -127,16 +127,16 @@ def make_int(ref_int, tag, *, batch, t_len, dims, act="softplus", no_inh=False,
     out.update(clip_u8=clips, label_u8=np.array([ord(b) for b in labels], np.uint8),
                cfg_cell=np.array("int"), cfg_act=np.array(act), cfg_no_inh=np.array(no_inh),
                cfg_lesion=np.array(",".join(lesion)), cfg_dims=np.array(dims),
-               cfg_k=np.array(7))
+               cfg_k=np.array(k))
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
     print(tag, {k: v.shape for k, v in out.items() if k in ("logits", "states", "gates")},
           "loss", float(out["loss"]))
 
 
-def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0, want_gates=True, hw=(32, 32)):
+def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0, want_gates=True, hw=(32, 32), k=7):
     synth = _synth()
     torch.manual_seed(2000 + seed)
-    model = ref_hgru.FFhGRU(dimensions=dims, timesteps=t_len, kernel_size=7,
+    model = ref_hgru.FFhGRU(dimensions=dims, timesteps=t_len, kernel_size=k,
                             jacobian_penalty=False, grad_method="bptt")
     perturb_recurrent(model, seed)
     clips, labels = synth.make_batch(seed + 7, batch, t_len, h=hw[0], w=hw[1])
@@ -144,7 +144,7 @@ def make_hgru(ref_hgru, tag, *, batch, t_len, dims, seed=0, want_gates=True, hw=
     out = run_recurrent(model, x, y, want_gates)
     out.update(clip_u8=clips, label_u8=np.array([ord(b) for b in labels], np.uint8),
                cfg_cell=np.array("hgru"), cfg_act=np.array("softplus"), cfg_no_inh=np.array(False),
-               cfg_lesion=np.array(""), cfg_dims=np.array(dims), cfg_k=np.array(7))
+               cfg_lesion=np.array(""), cfg_dims=np.array(dims), cfg_k=np.array(k))
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
     print(tag, "loss", float(out["loss"]))
 
@@ -308,6 +308,15 @@ def main():
                                          seed=11, hw=(64, 64)),
             "int_64x96": lambda: make_int(ref_int, "int_64x96", batch=2, t_len=3, dims=32,
                                           seed=12, hw=(64, 96)),
+            # the constructors' default kernel_size=15 (InT.py:184, ffhgru_hierarchy.py:178;
+            # the engine passes 7), an odd size between, and channel counts < 32
+            "int_k15": lambda: make_int(ref_int, "int_k15", batch=2, t_len=5, dims=32, seed=13,
+                                        k=15),
+            "int_k9_c16": lambda: make_int(ref_int, "int_k9_c16", batch=3, t_len=4, dims=16,
+                                           seed=14, k=9),
+            "hgru_k15_64": lambda: make_hgru(ref_hgru, "hgru_k15_64", batch=1, t_len=3, dims=32,
+                                             seed=15, hw=(64, 64), k=15),
+            "hgru_c24": lambda: make_hgru(ref_hgru, "hgru_c24", batch=2, t_len=4, dims=24, seed=16),
             # feedforward / recurrent comparison baselines (BASELINE configs[4])
             "gru_c16": lambda: make_gru(ref_kys, "gru_c16", batch=2, t_len=4, dims=16, seed=1),
             "r3d_small": lambda: make_r3d(ref_r3d, "r3d_small", batch=2, t_len=4, seed=2),

@@ -27,4 +27,4 @@ def prepared_input(g):
 def cfg(g):
     return dict(cell=str(g["cfg_cell"]), act=str(g["cfg_act"]), no_inh=bool(g["cfg_no_inh"]),
                 lesion=[s for s in str(g["cfg_lesion"]).split(",") if s],
-                dims=int(g["cfg_dims"]))
+                dims=int(g["cfg_dims"]), k=int(g["cfg_k"]) if "cfg_k" in g else 7)

@@ -140,3 +140,49 @@ def test_headline_size_permutation_and_reproducibility():
     for k, p in m.named_parameters():
         if p.grad is not None:                           # the mean loss is permutation invariant
             _close(f"permuted grad {k}", p.grad, g1[k], 1e-6, 2e-3)
+
+
+@pytest.mark.parametrize("cls,kw,hw", [("int", {}, 32), ("int", {"dimensions": 20, "kernel_size": 11}, 32),
+                                      ("hgru", {"kernel_size": 13}, 64)])
+def test_constructor_defaults_and_other_sizes(cls, kw, hw):
+    """The reference constructors' defaults (kernel_size=15, InT.py:184 /
+    ffhgru_hierarchy.py:178) and other (C, k) pairs against the CPU oracle."""
+    from models import InT, ffhgru_hierarchy as hg
+    mod = hg.FFhGRU if cls == "hgru" else InT.InT
+    args = {"dimensions": 32, **kw}
+    torch.manual_seed(17)
+    m = mod(args.pop("dimensions"), 3, **args)
+    assert m.kernel_size == kw.get("kernel_size", 15)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
+                p.uniform_(0.5, 1.5)
+            elif n.endswith(("mu", "gamma")):
+                p.uniform_(-0.5, 0.5)
+    x, y = _batch(61, 2, 3, hw=hw)
+    _vs_oracle(m, x, y, hgru=cls == "hgru")
+
+
+def test_k15_bf16_close_to_f32():
+    """bf16 cell at the constructors' default k = 15: logits and gradient
+    directions against the f32 cell (same parameters and clips)."""
+    from models import InT
+    dev = _dev()
+    torch.manual_seed(19)
+    m = InT.InT(32, 6).to(dev)
+    x, y = _batch(63, 8, 6)
+    x, y = x.to(dev), y.to(dev).reshape(-1, 1)
+    res = {}
+    for dt in ("f32", "bf16"):
+        m.cell_dtype = dt
+        m.zero_grad(set_to_none=True)
+        out, _ = m(x)
+        F.binary_cross_entropy_with_logits(out, y).backward()
+        res[dt] = (out.detach().double(), {k: p.grad.detach().double().flatten()
+                                           for k, p in m.named_parameters() if p.grad is not None})
+    (o32, g32), (o16, g16) = res["f32"], res["bf16"]
+    assert float((o16 - o32).abs().max()) < 5e-2
+    for k in g32:
+        if g32[k].norm() > 1e-12:
+            cos = float(g16[k] @ g32[k] / (g16[k].norm() * g32[k].norm()))
+            assert cos > 0.99, (k, cos)

@@ -14,8 +14,11 @@ from goldens import cfg, load, params, prepared_input
 
 pytestmark = pytest.mark.gpu
 
-INT_TAGS = ["int_c32", "int_tanh", "int_lesion", "int_noinh", "int_cfg1", "int_64x96"]
-HGRU_TAGS = ["hgru_c32", "hgru_b4t16", "hgru_64"]
+# k = 7 (the engine's), the constructors' default k = 15 and k = 9; C = 32 and
+# C < 32 (zero-padded to the MFMA tile inside the library)
+INT_TAGS = ["int_c32", "int_tanh", "int_lesion", "int_noinh", "int_cfg1", "int_64x96",
+            "int_tiny_c8", "int_k15", "int_k9_c16"]
+HGRU_TAGS = ["hgru_c32", "hgru_b4t16", "hgru_64", "hgru_k15_64", "hgru_c24"]
 
 
 def _dev():
@@ -30,11 +33,11 @@ def _model(g, dtype="f32"):
     c = cfg(g)
     if c["cell"] == "hgru":
         from models import ffhgru_hierarchy as hg
-        m = hg.FFhGRU(dimensions=c["dims"], timesteps=8, kernel_size=7)
+        m = hg.FFhGRU(dimensions=c["dims"], timesteps=8, kernel_size=c["k"])
         m.load_state_dict(params(g), strict=True)
         m.cell_dtype = dtype
         return m
-    kw = dict(dimensions=c["dims"], timesteps=8, kernel_size=7, no_inh=c["no_inh"],
+    kw = dict(dimensions=c["dims"], timesteps=8, kernel_size=c["k"], no_inh=c["no_inh"],
               nl=F.tanh if c["act"] == "tanh" else F.softplus)
     for les in c["lesion"]:
         kw["lesion_" + les] = True

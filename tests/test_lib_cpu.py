@@ -54,12 +54,21 @@ def test_size_queries_and_validation():
     frame = 256 * 1024 * 32 * 2
     assert saved >= 6 * 64 * frame          # six per-frame tensors kept for BPTT
     assert lib.pt_cell_workspace_bytes(ctypes.byref(d)) >= 2 * 64 * frame
-    bad = _lib.Desc(batch=2, channels=16, frames=8, height=32, width=32, ksize=7, act=0,
+    bad = _lib.Desc(batch=2, channels=33, frames=8, height=32, width=32, ksize=7, act=0,
                     no_inh=0, cell=0, dtype=0, eps=1e-3)
     assert lib.pt_cell_saved_bytes(ctypes.byref(bad)) == 0
     assert b"channels" in lib.pt_last_error()
-    bad.channels, bad.ksize = 32, 4
-    assert lib.pt_cell_saved_bytes(ctypes.byref(bad)) == 0
+    for k in (4, 17):                        # odd, <= 15 (the constructors' default is 15)
+        bad.channels, bad.ksize = 32, k
+        assert lib.pt_cell_saved_bytes(ctypes.byref(bad)) == 0
+        assert b"ksize" in lib.pt_last_error()
+    # C < 32 runs zero-padded (the padded parameter copies live in the saved blob);
+    # k = 9..15 uses the 46 x 46 tile and K*K-tap weight fragments
+    ok = _lib.Desc(batch=2, channels=8, frames=8, height=32, width=32, ksize=15, act=0,
+                   no_inh=0, cell=0, dtype=0, eps=1e-3)
+    assert lib.pt_cell_saved_bytes(ctypes.byref(ok)) > 0
+    ok.channels = 32
+    assert lib.pt_cell_saved_bytes(ctypes.byref(ok)) > 0
     # frames larger than 32x32 run as 32x32 tiles: sizes scale with the tile count
     # (cfg4: hGRU 64x64x128f, 128 clips per GPU); sides must be multiples of 32
     big = _lib.Desc(batch=128, channels=32, frames=128, height=64, width=64, ksize=7, act=0,

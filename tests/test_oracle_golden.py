@@ -12,7 +12,8 @@ from oracle import cells
 from goldens import cfg, load, params, prepared_input
 
 RECURRENT = ["int_tiny_c8", "int_c32", "int_noinh", "int_tanh", "int_lesion", "int_cfg1",
-             "hgru_c32", "hgru_b4t16", "hgru_64", "int_64x96"]
+             "hgru_c32", "hgru_b4t16", "hgru_64", "int_64x96", "int_k15", "int_k9_c16",
+             "hgru_k15_64", "hgru_c24"]
 
 
 def _close(a, b, rtol=2e-5, atol=2e-6):
