@@ -44,6 +44,11 @@ typedef struct pt_lstm_desc {
     int32_t steps;        /* recurrent steps T (timesteps), >= 1               */
     int32_t dtype;        /* PT_LSTM_F32 / PT_LSTM_BF16                        */
     int32_t init_state;   /* PT_LSTM_H0 | PT_LSTM_C0: initial h / c are given  */
+    int32_t x_seq;        /* 0: static x [B,cin,H,W] (the reference ConvLSTM,
+                             convlstm.py:137-143, recurs on one image);
+                             1: one input per step, x [B,cin,T,H,W], x_t =
+                             x[:, :, t] (the video adaptation for PathTracker
+                             clips)                           */
 } pt_lstm_desc;
 
 /* fp32, PyTorch layouts: wx[g] [ch,cin,k,k], bx[g] [ch], wh[g] [ch,ch,k,k]. */
@@ -53,7 +58,7 @@ typedef struct pt_lstm_params {
     const float* wh[4];
 } pt_lstm_params;
 
-/* Gradients (fp32, overwritten; any pointer may be NULL).  d_x [B,cin,H,W];
+/* Gradients (fp32, overwritten; any pointer may be NULL).  d_x shaped like x;
  * d_h0 / d_c0 [B,ch,H,W] (only meaningful when h0 / c0 were given). */
 typedef struct pt_lstm_grads {
     float* wx[4];
@@ -67,7 +72,8 @@ typedef struct pt_lstm_grads {
 size_t pt_lstm_saved_bytes(const pt_lstm_desc* d);
 size_t pt_lstm_workspace_bytes(const pt_lstm_desc* d);
 
-/* T steps of the cell on a static x [B,cin,H,W] from (h0, c0) [B,ch,H,W]
+/* T steps of the cell on x (static [B,cin,H,W], or per step [B,cin,T,H,W] when
+ * desc.x_seq) from (h0, c0) [B,ch,H,W]
  * (NULL = zeros, as convlstm.py:120-121; must agree with desc.init_state).
  * Writes h_T, c_T [B,ch,H,W] (either may be NULL) and keeps everything the
  * backward / jv calls need in `saved` (prepared weight fragments included). */

@@ -233,3 +233,41 @@ def flops_per_clip_frame(c: int = 32, h: int = 32, w: int = 32, k: int = 7) -> i
 
 def param_count(sd: Params) -> int:
     return int(sum(math.prod(v.shape) for v in sd.values()))
+
+
+def convlstm_video_forward(sd: Params, x: Tensor, act: str = "softplus"):
+    """The ConvLSTM clip model (repo models/convlstm.py ConvLSTMVideo, DESIGN.md
+    §10), restated with stock torch ops: the InT stem per frame
+    (models/InT.py:212-213), the reference ConvLSTMCell step
+    (models/convlstm.py:84-90) with the frame as its input, and InT's readout
+    (models/InT.py:236-241) on h_T.  Returns ``(logits [B,1], h_T, hs, cs)``."""
+    nl = F.softplus if act == "softplus" else torch.tanh
+    xbn = nl(F.conv3d(x, sd["preproc.weight"], sd["preproc.bias"]))
+    k = sd["unit1.Wxi.weight"].shape[-1]
+    pad = (k - 1) // 2
+    b, ch, t_len, hh, ww = xbn.shape
+    h = torch.zeros((b, ch, hh, ww), dtype=x.dtype)
+    c = torch.zeros_like(h)
+
+    def xconv(g, v):
+        return F.conv2d(v, sd[f"unit1.Wx{g}.weight"], sd[f"unit1.Wx{g}.bias"], padding=pad)
+
+    def hconv(g, v):
+        return F.conv2d(v, sd[f"unit1.Wh{g}.weight"], None, padding=pad)
+
+    hs, cs = [], []
+    for t in range(t_len):
+        xt = xbn[:, :, t]
+        i_t = torch.sigmoid(xconv("i", xt) + hconv("i", h))
+        f_t = torch.sigmoid(xconv("f", xt) + hconv("f", h))
+        c = f_t * c + i_t * torch.tanh(xconv("c", xt) + hconv("c", h))
+        o_t = torch.sigmoid(xconv("o", xt) + hconv("o", h))
+        h = o_t * torch.tanh(c)
+        hs.append(h)
+        cs.append(c)
+    o = torch.cat([F.conv2d(h, sd["readout_conv.weight"], sd["readout_conv.bias"]),
+                   x[:, 2, 0][:, None]], 1)
+    o = F.conv2d(o, sd["target_conv.weight"], sd["target_conv.bias"], padding=2)
+    o = F.avg_pool2d(o, kernel_size=o.size()[2:])
+    o = F.linear(o.reshape(b, -1), sd["readout_dense.weight"], sd["readout_dense.bias"])
+    return o, h, hs, cs

@@ -564,21 +564,24 @@ __global__ void k_lreduce(LReduceArgs r) {
 }
 
 // ------------------------------------------------------------ conversions
-// NCHW fp32 [B][nc][NPIX] -> channels-last [B][NPIX][32] (zero padded)
+// NCHW fp32 [B][nc][NPIX] -> channels-last [B][NPIX][32] (zero padded).
+// tn > 1: frame t of [B][nc][tn][NPIX] (x_seq inputs / their gradients).
 template <class S>
-__global__ void k_to_cl(const float* __restrict__ src, S* __restrict__ dst, int B, int nc) {
+__global__ void k_to_cl(const float* __restrict__ src, S* __restrict__ dst, int B, int nc,
+                        int tn = 1, int t = 0) {
   const int n = B * NPIX * HC;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int c = e % HC, pix = (e / HC) % NPIX, b = e / (HC * NPIX);
-    dst[e] = (S)(c < nc ? src[((size_t)b * nc + c) * NPIX + pix] : 0.f);
+    dst[e] = (S)(c < nc ? src[(((size_t)b * nc + c) * tn + t) * NPIX + pix] : 0.f);
   }
 }
 template <class S>
-__global__ void k_from_cl(const S* __restrict__ src, float* __restrict__ dst, int B, int nc) {
+__global__ void k_from_cl(const S* __restrict__ src, float* __restrict__ dst, int B, int nc,
+                          int tn = 1, int t = 0) {
   const int n = B * nc * NPIX;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int pix = e % NPIX, c = (e / NPIX) % nc, b = e / (NPIX * nc);
-    dst[e] = ldf(src + ((size_t)b * NPIX + pix) * HC + c);
+    dst[(((size_t)b * nc + c) * tn + t) * NPIX + pix] = ldf(src + ((size_t)b * NPIX + pix) * HC + c);
   }
 }
 
@@ -645,6 +648,7 @@ inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct LPlan {
   int B, T, K, ch, cin, nsl_h, nsl_x, nb;
+  int xseq;           // one input image per step (desc.x_seq)
   size_t es, npix;
   // saved
   size_t o_fr[4], o_bias, o_x, o_xg, o_h0, o_c0, o_P, o_h, o_c, saved;
@@ -664,6 +668,7 @@ int check(const pt_lstm_desc* d) {
     return fail(PT_LSTM_ERR_UNSUPPORTED, "ksize must be odd and <= 15 (got %ld)", d->ksize);
   if (d->batch < 1 || d->steps < 1) return fail(PT_LSTM_ERR_ARG, "batch and steps must be >= 1%ld");
   if (d->dtype != PT_LSTM_F32 && d->dtype != PT_LSTM_BF16) return fail(PT_LSTM_ERR_ARG, "bad dtype%ld");
+  if (d->x_seq != 0 && d->x_seq != 1) return fail(PT_LSTM_ERR_ARG, "bad x_seq (%ld)", d->x_seq);
   return 0;
 }
 
@@ -682,7 +687,8 @@ LPlan plan(const pt_lstm_desc* d) {
   size_t o = 0;
   for (int i = 0; i < 4; ++i) { p.o_fr[i] = o; o += al(NG * KK * 1024 * p.es); }
   p.o_bias = o; o += al(GC * 4);
-  p.o_x = o; o += al(p.npix * HC * p.es);
+  p.xseq = d->x_seq != 0;
+  p.o_x = o; o += al(p.npix * HC * p.es * (p.xseq ? p.T : 1));   // [steps][B][NPIX][32]
   p.o_xg = o; o += al(p.npix * GC * 4);
   p.o_h0 = o; o += al(p.npix * HC * p.es);
   p.o_c0 = o; o += al(p.npix * HC * 4);
@@ -691,7 +697,7 @@ LPlan plan(const pt_lstm_desc* d) {
   p.o_c = o; o += al(p.npix * HC * 4 * p.T);
   p.saved = o;
   p.nsl_h = slices(p.B * p.T, p.K);
-  p.nsl_x = slices(p.B, p.K);
+  p.nsl_x = slices(p.xseq ? p.B * p.T : p.B, p.K);
   p.nb = 256;
   o = 0;
   p.o_dh = o; o += al(2 * p.npix * HC * 4);
@@ -809,7 +815,10 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   HIPCHK(hipGetLastError());
 
   S* xcl = (S*)(sv + p.o_x);
-  hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, x, xcl, p.B, p.cin);
+  const size_t hstep0 = p.npix * HC;
+  for (int t = 0; t < (p.xseq ? p.T : 1); ++t)
+    hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, x, xcl + t * hstep0,
+                       p.B, p.cin, p.xseq ? p.T : 1, t);
   S* hinit = h0 ? (S*)(sv + p.o_h0) : nullptr;
   float* cinit = c0 ? (float*)(sv + p.o_c0) : nullptr;
   if (h0) hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, h0, hinit, p.B, p.ch);
@@ -820,12 +829,20 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   S* H = (S*)(sv + p.o_h);
   float* Cc = (float*)(sv + p.o_c);
   const size_t pstep = p.npix * GC, hstep = p.npix * HC;
+  // static x: xg = Wx*x + b once, P_t = xg + Wh*h_{t-1}; per-step x:
+  // P_t = Wx*x_t + b, then += Wh*h_{t-1} in place
   float* xg = h0 ? (float*)(sv + p.o_xg) : P;      // without h0, P_0 = xg
-  if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], xg, nullptr, pa.bias, p.B, st)) return rc;
+  if (!p.xseq)
+    if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], xg, nullptr, pa.bias, p.B, st)) return rc;
   for (int t = 0; t < p.T; ++t) {
     const S* hin = t == 0 ? hinit : H + (t - 1) * hstep;
+    if (p.xseq)
+      if (int rc = conv_k<S, 1, 4>(p.K, xcl + t * hstep, sv + p.o_fr[0], P + t * pstep, nullptr,
+                                   pa.bias, p.B, st))
+        return rc;
     if (hin)
-      if (int rc = conv_k<S, 1, 4>(p.K, hin, sv + p.o_fr[1], P + t * pstep, xg, nullptr, p.B, st))
+      if (int rc = conv_k<S, 1, 4>(p.K, hin, sv + p.o_fr[1], P + t * pstep,
+                                   p.xseq ? P + t * pstep : xg, nullptr, p.B, st))
         return rc;
     const float* cprev = t == 0 ? cinit : Cc + (t - 1) * hstep;
     hipLaunchKernelGGL(k_lpw_fwd<S>, grid_for((size_t)npix * 8), dim3(256), 0, st,
@@ -892,7 +909,9 @@ int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
   wa.wslab = (float*)(ws + p.o_wsh);
   if (int rc = wgrad_k<S>(p.K, wa, st)) return rc;
   LWgradArgs wx{};
-  wx.X0 = sv + p.o_x; wx.D0 = dPsumS; wx.n0 = p.B;
+  // static x: one image against sum_t dP_t; per-step x: every (x_t, dP_t)
+  wx.X0 = sv + p.o_x; wx.D0 = p.xseq ? (const void*)dP : (const void*)dPsumS;
+  wx.n0 = p.xseq ? p.B * p.T : p.B;
   wx.X1 = nullptr; wx.D1 = nullptr; wx.n1 = 0;
   wx.nsl = p.nsl_x;
   wx.wslab = (float*)(ws + p.o_wsx);
@@ -906,9 +925,13 @@ int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
   hipLaunchKernelGGL(k_lreduce, dim3(1024), dim3(256), 0, st, ra);
   HIPCHK(hipGetLastError());
   if (g->d_x) {
-    if (int rc = conv_k<S, 4, 1>(p.K, dPsumS, sv + p.o_fr[3], dh, nullptr, nullptr, p.B, st)) return rc;
-    hipLaunchKernelGGL(k_from_cl<float>, grid_for(p.npix * p.cin), dim3(256), 0, st,
-                       (const float*)dh, g->d_x, p.B, p.cin);
+    for (int t = 0; t < (p.xseq ? p.T : 1); ++t) {
+      if (int rc = conv_k<S, 4, 1>(p.K, p.xseq ? (const void*)(dP + t * pstep) : (const void*)dPsumS,
+                                   sv + p.o_fr[3], dh, nullptr, nullptr, p.B, st))
+        return rc;
+      hipLaunchKernelGGL(k_from_cl<float>, grid_for(p.npix * p.cin), dim3(256), 0, st,
+                         (const float*)dh, g->d_x, p.B, p.cin, p.xseq ? p.T : 1, t);
+    }
     HIPCHK(hipGetLastError());
   }
   return 0;

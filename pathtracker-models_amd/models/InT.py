@@ -161,3 +161,30 @@ class InT(nn.Module):
             return output, states, gates
         jv_penalty = torch.ones(1, device=x.device)
         return output, jv_penalty
+
+
+class FC(nn.Module):
+    """Feed-forward control of the reference (models/InT.py:248-271; registry
+    'fc', utils/engine.py:154-161): 1x1x1 conv stem, BatchNorm3d with batch
+    statistics, one Linear over the whole clip.  Plain PyTorch (MIOpen /
+    hipBLASLt on the GPU): it is a comparison model, not the recurrent hot
+    path.  The Linear is sized for 64-frame 32x32 clips with 32 channels, as in
+    the reference (``nn.Linear(64*32*32*32, 1)``, :260)."""
+
+    def __init__(self, dimensions, timesteps=8, kernel_size=15, jacobian_penalty=False,
+                 grad_method='bptt'):
+        super().__init__()
+        self.timesteps = timesteps
+        self.jacobian_penalty = jacobian_penalty
+        self.grad_method = grad_method
+        self.hgru_size = dimensions
+        self.bn = nn.BatchNorm3d(self.hgru_size, eps=1e-03, track_running_stats=False)
+        self.preproc = nn.Conv3d(3, dimensions, kernel_size=1)
+        self.readout = nn.Linear(64 * 32 * 32 * 32, 1)
+
+    def forward(self, x, testmode=False):
+        x = self.preproc(x)
+        x = self.bn(x)
+        x = self.readout(x.reshape(x.shape[0], -1))
+        jv_penalty = torch.ones(1, device=x.device)
+        return x, jv_penalty

@@ -26,6 +26,7 @@ import os
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 from torch.autograd import Function
 from torch.nn import init
 
@@ -191,3 +192,70 @@ class ConvLSTM(nn.Module):
         if testmode:
             return output, states, loss
         return output, jv_penalty, loss
+
+
+class ConvLSTMVideo(nn.Module):
+    """ConvLSTM on PathTracker clips: BASELINE configs[2] ("ConvLSTM ... same
+    clips").  Not a reference class: the reference ConvLSTM recurs on ONE static
+    image (convlstm.py:116-147), so the clip version is defined here
+     from the reference's own parts:
+
+    * stem      ``nl(Conv3d 1x1x1 3->C)`` per frame, as InT (InT.py:192,212-213);
+    * recurrence ``ConvLSTMCell`` (convlstm.py:84-90) with the frame as input:
+                 h_t, c_t = cell(x_t, h_{t-1}, c_{t-1}), h_0 = c_0 = 0; the
+                 x-convs see a new frame each step (the library's x_seq mode);
+    * readout   InT's (InT.py:236-241) on h_T: readout_conv C->1, the target
+                 marker x[:, 2, 0], target_conv 5x5, global average, Linear(1,1);
+    * jv_penalty the reference ConvLSTM's training-mode Jacobian penalty of the
+                 last step (convlstm.py:150-161), detached, as ``ConvLSTM``.
+
+    ``forward(x, testmode=False)`` has InT's signature and returns
+    ``(logits [B,1], jv_penalty)``, so engine.model_step / mainclean.py run it
+    (registry name ``convlstm``).
+    """
+
+    def __init__(self, dimensions=25, timesteps=8, kernel_size=7, jacobian_penalty=False,
+                 grad_method='bptt', nl=F.softplus):
+        super().__init__()
+        if grad_method != 'bptt':
+            raise NotImplementedError("ConvLSTMVideo trains with BPTT only")
+        self.timesteps = timesteps
+        self.jacobian_penalty = jacobian_penalty
+        self.grad_method = grad_method
+        self.hgru_size = dimensions
+        self.kernel_size = kernel_size
+        self.nl = nl
+        self.preproc = nn.Conv3d(3, dimensions, kernel_size=1)
+        self.unit1 = ConvLSTMCell(dimensions, dimensions, kernel_size)
+        self.readout_conv = nn.Conv2d(dimensions, 1, 1)
+        self.target_conv = nn.Conv2d(2, 1, 5, padding=2)
+        init.zeros_(self.target_conv.bias)
+        self.readout_dense = nn.Linear(1, 1)
+
+    @property
+    def cell_dtype(self):
+        return self.unit1.cell_dtype
+
+    @cell_dtype.setter
+    def cell_dtype(self, v):
+        self.unit1.cell_dtype = v
+
+    def forward(self, x, testmode=False):
+        if testmode:
+            raise NotImplementedError("ConvLSTMVideo has no per-frame testmode outputs")
+        # the 1x1x1 stem as a batched [C x 3] @ [3 x T*H*W] product: MIOpen's
+        # Conv3d path for it ran naive kernels over the 1.7 GB stem output
+        # (2.5 s/step at B=256, T=64), einsum's permuted GEMM ~25 ms
+        b, _, t, hh, ww = x.shape
+        w = self.preproc.weight.reshape(self.hgru_size, 3)
+        z = torch.matmul(w, x.reshape(b, 3, t * hh * ww)) + self.preproc.bias[:, None]
+        xbn = self.nl(z).reshape(b, self.hgru_size, t, hh, ww)   # [B, C, T, H, W]
+        steps = xbn.shape[2]
+        want_jv = self.training and steps >= 2
+        h_t, _, jv = self.unit1.steps(xbn, steps, want_jv=want_jv)
+        out = torch.cat([self.readout_conv(h_t), x[:, 2, 0][:, None]], 1)
+        out = self.target_conv(out)
+        out = F.avg_pool2d(out, kernel_size=out.size()[2:])
+        out = self.readout_dense(out.reshape(x.shape[0], -1))
+        jv_penalty = jv if want_jv else torch.ones(1, device=x.device)
+        return out, jv_penalty

@@ -1,7 +1,8 @@
 """ctypes binding of ``libptlstm.so`` (include/pt_lstm.h) and its autograd bridge.
 
-``LSTMStepsFn`` runs ``steps`` ConvLSTM steps on a static input through the
-HIP library — forward, BPTT backward and (for the model's training mode) the
+``LSTMStepsFn`` runs ``steps`` ConvLSTM steps on a static input (the
+reference's form) or on one input image per step (``x`` [B,cin,T,H,W], the
+video adaptation for PathTracker clips) through the HIP library — forward, BPTT backward and (for the model's training mode) the
 Jacobian penalty — with every buffer owned by torch and the library seeing raw
 device pointers plus the current HIP stream.  It replaces, for the reference's
 ``models/convlstm.py``, the per-step Python loop (:137-143, cell :84-90) and
@@ -35,7 +36,7 @@ class Desc(ctypes.Structure):
                 ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("ksize", ctypes.c_int32),
                 ("steps", ctypes.c_int32), ("dtype", ctypes.c_int32),
-                ("init_state", ctypes.c_int32)]
+                ("init_state", ctypes.c_int32), ("x_seq", ctypes.c_int32)]
 
 
 class Params(ctypes.Structure):
@@ -94,11 +95,17 @@ DTYPES = {"f32": PT_LSTM_F32, "fp32": PT_LSTM_F32, "float32": PT_LSTM_F32,
 
 
 def make_desc(x, channels: int, ksize: int, steps: int, dtype: str, h0=None, c0=None) -> Desc:
-    b, cin, h, w = x.shape
+    """x: static [B,cin,H,W] or per step [B,cin,T,H,W] (T == steps)."""
+    if x.dim() == 5:
+        b, cin, t, h, w = x.shape
+        if t != steps:
+            raise ValueError(f"per-step input has {t} frames but steps={steps}")
+    else:
+        b, cin, h, w = x.shape
     return Desc(batch=b, in_channels=cin, channels=channels, height=h, width=w, ksize=ksize,
                 steps=steps, dtype=DTYPES[dtype],
                 init_state=(PT_LSTM_H0 if h0 is not None else 0)
-                | (PT_LSTM_C0 if c0 is not None else 0))
+                | (PT_LSTM_C0 if c0 is not None else 0), x_seq=int(x.dim() == 5))
 
 
 def _ptr(t):
@@ -143,7 +150,7 @@ class LSTMStepsFn(torch.autograd.Function):
         if nsaved == 0:
             check(1)
         saved = torch.empty(nsaved, dtype=torch.uint8, device=x.device)
-        b, _, hh, ww = x.shape
+        b, hh, ww = x.shape[0], x.shape[-2], x.shape[-1]
         h_out = torch.empty((b, ch, hh, ww), dtype=torch.float32, device=x.device)
         c_out = torch.empty_like(h_out)
         pp = Params()
@@ -162,6 +169,7 @@ class LSTMStepsFn(torch.autograd.Function):
             check(lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
                                          _ptr(jv), st))
         ctx.meta = (ksize, steps, dtype, h0 is not None, c0 is not None, tuple(x.shape), ch)
+        ctx.desc = d
         ctx.saved_blob = saved
         ctx.wshapes = [w.shape for w in weights]
         ctx.mark_non_differentiable(jv)
@@ -175,11 +183,9 @@ class LSTMStepsFn(torch.autograd.Function):
         # so the saved blob stays with ctx until autograd frees the graph
         lib = load()
         ksize, steps, dtype, has_h0, has_c0, xshape, ch = ctx.meta
-        b, cin, hh, ww = xshape
+        b, hh, ww = xshape[0], xshape[-2], xshape[-1]
         dev = ctx.saved_blob.device
-        d = Desc(batch=b, in_channels=cin, channels=ch, height=hh, width=ww, ksize=ksize,
-                 steps=steps, dtype=DTYPES[dtype],
-                 init_state=(PT_LSTM_H0 if has_h0 else 0) | (PT_LSTM_C0 if has_c0 else 0))
+        d = ctx.desc
         if d_h is None:
             d_h = torch.zeros((b, ch, hh, ww), device=dev)
         d_h = d_h.contiguous().float()

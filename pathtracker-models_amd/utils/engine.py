@@ -26,6 +26,7 @@ import torch.nn.functional as F
 
 from models import InT
 from models import ffhgru_hierarchy
+from models import convlstm
 from models import kys
 from models import nostridetv_cc_smallest
 
@@ -81,6 +82,12 @@ def model_selector(args, timesteps, device, fb_kernel_size=7, dimensions=32):
     if args.model == 'nostride_video_cc_small':  # engine.py:204-206 (comparison baseline)
         return nostridetv_cc_smallest.r3d_18(pretrained=getattr(args, 'pretrained', False),
                                              timesteps=timesteps)
+    if args.model == 'fc':                       # engine.py:154-161 (feed-forward control)
+        return InT.FC(dimensions=dimensions, timesteps=timesteps, kernel_size=fb_kernel_size,
+                      jacobian_penalty=False, grad_method='bptt')
+    if args.model == 'convlstm':                 # BASELINE configs[2]: ConvLSTM on the clips
+        return convlstm.ConvLSTMVideo(dimensions=25, timesteps=timesteps,
+                                      kernel_size=fb_kernel_size, grad_method='bptt')
     if args.model == 'ffhgru':
         return ffhgru_hierarchy.FFhGRU(dimensions=dimensions, timesteps=timesteps,
                                        kernel_size=fb_kernel_size, jacobian_penalty=False,

@@ -1,0 +1,88 @@
+"""ConvLSTM on PathTracker clips (BASELINE configs[2], models/convlstm.py
+ConvLSTMVideo): the library's per-step-input mode (x_seq)
+against the CPU restatement oracle/cells.py:convlstm_video_forward (f32,
+1e-3), the Jacobian penalty on that same trajectory, and bf16 within the
+stated tolerance.  Parity of the video model itself is against this repo's
+definition (the reference has no clip ConvLSTM); its cell step is the
+reference's and is pinned by the convlstm_* goldens (test_gpu_lstm.py)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def _clips(seed, b, t):
+    from ptamd import synth
+    clips, labels = synth.make_batch(seed, b, t)
+    x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float()
+    return x, torch.tensor([ord(v) for v in labels], dtype=torch.float32)
+
+
+def _model(k, seed):
+    from models import convlstm
+    torch.manual_seed(seed)
+    m = convlstm.ConvLSTMVideo(dimensions=25, timesteps=6, kernel_size=k)
+    with torch.no_grad():                                  # off the near-constant init
+        m.readout_conv.weight.mul_(8.0)
+        m.preproc.weight.mul_(2.0)
+    return m
+
+
+@pytest.mark.parametrize("k,b,t", [(7, 3, 6), (15, 2, 4), (3, 4, 2)])
+def test_video_convlstm_matches_oracle(k, b, t):
+    from oracle import cells
+    dev = _dev()
+    m = _model(k, 30 + k)
+    x, y = _clips(40 + k, b, t)
+    sd = {n: p.detach().clone().requires_grad_() for n, p in m.named_parameters()}
+    lo, _, hs, cs = cells.convlstm_video_forward(sd, x)
+    jr = cells.convlstm_jv_penalty(hs, cs) if t >= 2 else None
+    F.binary_cross_entropy_with_logits(lo, y.reshape(-1, 1)).backward()
+    m = m.to(dev).train()
+    out, jv = m(x.to(dev))
+    F.binary_cross_entropy_with_logits(out, y.to(dev).reshape(-1, 1)).backward()
+    assert float((out.detach().cpu() - lo.detach()).abs().max()) < 1e-3
+    for n, p in m.named_parameters():
+        r = sd[n].grad
+        err = float((p.grad.cpu() - r).abs().max())
+        assert err <= 1e-6 + 1e-3 * float(r.abs().max()), (n, err)
+    # the reference ConvLSTM's Jacobian penalty of the last step, on this trajectory
+    if t >= 2:
+        assert jv.shape == jr.shape
+        err = float((jv.cpu() - jr).abs().max())
+        assert err <= 1e-3 * (1.0 + float(jr.abs().max())), err
+
+
+def test_video_convlstm_bf16_tolerance():
+    dev = _dev()
+    m = _model(7, 5).to(dev).train()
+    x, y = _clips(9, 16, 8)
+    x, y = x.to(dev), y.to(dev).reshape(-1, 1)
+    res = {}
+    for dt in ("f32", "bf16"):
+        m.cell_dtype = dt
+        m.zero_grad(set_to_none=True)
+        out, _ = m(x)
+        F.binary_cross_entropy_with_logits(out, y).backward()
+        res[dt] = (out.detach().double(), {n: p.grad.detach().double().flatten()
+                                           for n, p in m.named_parameters()})
+    (o32, g32), (o16, g16) = res["f32"], res["bf16"]
+    assert float((o16 - o32).abs().max()) < 2e-2
+    for n in g32:
+        if g32[n].norm() > 1e-12:
+            cos = float(g16[n] @ g32[n] / (g16[n].norm() * g32[n].norm()))
+            assert cos > 0.99, (n, cos)
+
+
+def test_registry_builds_it():
+    import types
+    from utils import engine
+    m = engine.model_selector(types.SimpleNamespace(model="convlstm"), timesteps=8, device="cpu")
+    assert type(m).__name__ == "ConvLSTMVideo" and m.kernel_size == 7
