@@ -29,6 +29,7 @@
 #include "pt_graph.h"
 #include "../../include/pt_lstm.h"
 
+#include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -628,6 +629,111 @@ __global__ void k_lprep(LPrepArgs p) {
   }
 }
 
+// ------------------------------------------------------------- frame stem
+// Clip ConvLSTM stem: y = softplus(W x + b) per voxel, a 1x1x1
+// channel mix of x [B][CIN][n] into y [B][cout][n]; softplus as torch's
+// (beta 1, threshold 20).  One thread per 4 voxels: 16-byte loads / stores,
+// each output plane written contiguously; HBM-bound (CIN + cout floats/voxel).
+__device__ __forceinline__ float softplus20(float z) { return z > 20.f ? z : log1pf(expf(z)); }
+__device__ __forceinline__ float dsoftplus20(float z, float g) {
+  if (z > 20.f) return g;
+  const float e = expf(z);
+  return g * e / (e + 1.f);
+}
+
+template <int CIN>
+__global__ __launch_bounds__(256) void k_stem_fwd(const float4* __restrict__ x, const float* __restrict__ w,
+                                                  const float* __restrict__ b, float4* __restrict__ y,
+                                                  int cout, long n4, long total4) {
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total4; e += (long)gridDim.x * blockDim.x) {
+    const long bi = e / n4, v = e - bi * n4;
+    float4 xi[CIN];
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) xi[k] = x[(bi * CIN + k) * n4 + v];
+    for (int o = 0; o < cout; ++o) {
+      float4 z = make_float4(b[o], b[o], b[o], b[o]);
+#pragma unroll
+      for (int k = 0; k < CIN; ++k) {
+        const float wk = w[o * CIN + k];
+        z.x += wk * xi[k].x; z.y += wk * xi[k].y; z.z += wk * xi[k].z; z.w += wk * xi[k].w;
+      }
+      y[(bi * cout + o) * n4 + v] =
+          make_float4(softplus20(z.x), softplus20(z.y), softplus20(z.z), softplus20(z.w));
+    }
+  }
+}
+
+// dW [cout][CIN], db [cout] of the stem from dy, z recomputed from x: per-block
+// partial sums part[block][32 * (CIN + 1)] (wave shuffles, then LDS across the
+// 4 waves), summed in fixed order by k_stem_reduce (deterministic).
+template <int CIN>
+__global__ __launch_bounds__(256) void k_stem_bwd(const float4* __restrict__ x, const float* __restrict__ w,
+                                                  const float* __restrict__ b, const float4* __restrict__ dy,
+                                                  float* __restrict__ part, int cout, long n4, long total4) {
+  constexpr int NA = 32 * (CIN + 1);
+  float acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = 0.f;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total4; e += (long)gridDim.x * blockDim.x) {
+    const long bi = e / n4, v = e - bi * n4;
+    float4 xi[CIN];
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) xi[k] = x[(bi * CIN + k) * n4 + v];
+#pragma unroll
+    for (int o = 0; o < 32; ++o) {
+      if (o < cout) {
+        float4 z = make_float4(b[o], b[o], b[o], b[o]);
+#pragma unroll
+        for (int k = 0; k < CIN; ++k) {
+          const float wk = w[o * CIN + k];
+          z.x += wk * xi[k].x; z.y += wk * xi[k].y; z.z += wk * xi[k].z; z.w += wk * xi[k].w;
+        }
+        const float4 d = dy[(bi * cout + o) * n4 + v];
+        const float gx = dsoftplus20(z.x, d.x), gy = dsoftplus20(z.y, d.y), gz = dsoftplus20(z.z, d.z),
+                    gw = dsoftplus20(z.w, d.w);
+#pragma unroll
+        for (int k = 0; k < CIN; ++k)
+          acc[o * (CIN + 1) + k] += (gx * xi[k].x + gy * xi[k].y) + (gz * xi[k].z + gw * xi[k].w);
+        acc[o * (CIN + 1) + CIN] += (gx + gy) + (gz + gw);
+      }
+    }
+  }
+  __shared__ float red[4][NA];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    float t = acc[i];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+    if (lane == 0) red[wv][i] = t;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NA; i += blockDim.x)
+    part[(size_t)blockIdx.x * NA + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
+// One workgroup per accumulator: 256 threads stride the partials, then a
+// fixed-order tree in LDS (deterministic), fp64 throughout.
+__global__ __launch_bounds__(256) void k_stem_reduce(const float* __restrict__ part, int nblk, int cin,
+                                                     int cout, float* __restrict__ dw, float* __restrict__ db) {
+  const int na = 32 * (cin + 1), i = blockIdx.x;
+  const int o = i / (cin + 1), k = i % (cin + 1);
+  if (o >= cout) return;                       // uniform per workgroup
+  double s = 0.0;
+  for (int j = threadIdx.x; j < nblk; j += blockDim.x) s += part[(size_t)j * na + i];
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int m = 128; m >= 1; m >>= 1) {
+    if (threadIdx.x < m) red[threadIdx.x] += red[threadIdx.x + m];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (k < cin) { if (dw) dw[o * cin + k] = (float)red[0]; }
+    else if (db) db[o] = (float)red[0];
+  }
+}
+
 }  // namespace ptl
 
 // =========================================================================
@@ -957,6 +1063,16 @@ int run_jv(const pt_lstm_desc* d, const char* sv, char* ws, float mu, float* jv,
   return 0;
 }
 
+constexpr int STEM_BLOCKS = 1024;
+
+int stem_check(const float* x, const float* w, int B, int cin, int cout, long long n) {
+  if (!x || !w) return fail(PT_LSTM_ERR_ARG, "null x / w%ld");
+  if (B < 1 || cin < 1 || cin > 4 || cout < 1 || cout > 32)
+    return fail(PT_LSTM_ERR_UNSUPPORTED, "stem needs B >= 1, cin 1..4, cout 1..32 (cin=%ld)", cin);
+  if (n < 4 || n % 4) return fail(PT_LSTM_ERR_UNSUPPORTED, "stem voxel count must be a multiple of 4 (%ld)", (long)n);
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1019,6 +1135,45 @@ int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace
   hipStream_t st = (hipStream_t)stream;
   return bf ? run_jv<bf16_t>(d, (const char*)saved, (char*)workspace, mu, jv, st)
             : run_jv<float>(d, (const char*)saved, (char*)workspace, mu, jv, st);
+}
+
+size_t pt_lstm_stem_workspace_bytes(int cin) {
+  return cin < 1 || cin > 4 ? 0 : (size_t)STEM_BLOCKS * 32 * (cin + 1) * sizeof(float);
+}
+
+int pt_lstm_stem_forward(const float* x, const float* w, const float* b, int B, int cin, int cout,
+                         long long n, float* y, pt_lstm_stream_t stream) {
+  if (int rc = stem_check(x, w, B, cin, cout, n)) return rc;
+  if (!b || !y) return fail(PT_LSTM_ERR_ARG, "null b / y%ld");
+  const long n4 = (long)(n / 4), total4 = (long)B * n4;
+  const int grid = (int)std::min<long>((total4 + 255) / 256, 8192);
+  hipStream_t st = (hipStream_t)stream;
+  switch (cin) {
+#define STEM_F(C) case C: hipLaunchKernelGGL(k_stem_fwd<C>, dim3(grid), dim3(256), 0, st, (const float4*)x, w, b, (float4*)y, cout, n4, total4); break;
+    STEM_F(1) STEM_F(2) STEM_F(3) STEM_F(4)
+#undef STEM_F
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int pt_lstm_stem_backward(const float* x, const float* w, const float* b, const float* dy, int B,
+                          int cin, int cout, long long n, void* workspace, float* dw, float* db,
+                          pt_lstm_stream_t stream) {
+  if (int rc = stem_check(x, w, B, cin, cout, n)) return rc;
+  if (!b || !dy || !workspace) return fail(PT_LSTM_ERR_ARG, "null b / dy / workspace%ld");
+  const long n4 = (long)(n / 4), total4 = (long)B * n4;
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  switch (cin) {
+#define STEM_B(C) case C: hipLaunchKernelGGL(k_stem_bwd<C>, dim3(STEM_BLOCKS), dim3(256), 0, st, (const float4*)x, w, b, (const float4*)dy, part, cout, n4, total4); break;
+    STEM_B(1) STEM_B(2) STEM_B(3) STEM_B(4)
+#undef STEM_B
+  }
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_stem_reduce, dim3(32 * (cin + 1)), dim3(256), 0, st, (const float*)part, STEM_BLOCKS, cin, cout, dw, db);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 const char* pt_lstm_last_error(void) { return g_err; }

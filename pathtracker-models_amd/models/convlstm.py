@@ -30,6 +30,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 from torch.nn import init
 
+from ptamd import lstm
 from ptamd.lstm import run_steps
 
 _DEFAULT_DTYPE = os.environ.get("PT_CELL_DTYPE", "f32")
@@ -219,6 +220,8 @@ class ConvLSTMVideo(nn.Module):
         super().__init__()
         if grad_method != 'bptt':
             raise NotImplementedError("ConvLSTMVideo trains with BPTT only")
+        if nl is not F.softplus:
+            raise NotImplementedError("the HIP stem fuses F.softplus (InT's default nl)")
         self.timesteps = timesteps
         self.jacobian_penalty = jacobian_penalty
         self.grad_method = grad_method
@@ -243,13 +246,9 @@ class ConvLSTMVideo(nn.Module):
     def forward(self, x, testmode=False):
         if testmode:
             raise NotImplementedError("ConvLSTMVideo has no per-frame testmode outputs")
-        # the 1x1x1 stem as a batched [C x 3] @ [3 x T*H*W] product: MIOpen's
-        # Conv3d path for it ran naive kernels over the 1.7 GB stem output
-        # (2.5 s/step at B=256, T=64), einsum's permuted GEMM ~25 ms
-        b, _, t, hh, ww = x.shape
-        w = self.preproc.weight.reshape(self.hgru_size, 3)
-        z = torch.matmul(w, x.reshape(b, 3, t * hh * ww)) + self.preproc.bias[:, None]
-        xbn = self.nl(z).reshape(b, self.hgru_size, t, hh, ww)   # [B, C, T, H, W]
+        # the 1x1x1 stem + softplus in one HBM pass (pt_lstm_stem_*); a
+        # [C x 3] @ [3 x THW] library GEMM took 16 ms of a 88 ms step here
+        xbn = lstm.stem(x, self.preproc.weight, self.preproc.bias)   # [B, C, T, H, W]
         steps = xbn.shape[2]
         want_jv = self.training and steps >= 2
         h_t, _, jv = self.unit1.steps(xbn, steps, want_jv=want_jv)

@@ -23,10 +23,13 @@ LIB_PATH = os.path.join(HERE, "libptlstm.so")
 
 PT_LSTM_F32, PT_LSTM_BF16 = 0, 1
 PT_LSTM_H0, PT_LSTM_C0 = 1, 2
+PT_LSTM_OK, PT_LSTM_ERR_ARG, PT_LSTM_ERR_UNSUPPORTED, PT_LSTM_ERR_HIP = 0, 1, 2, 3
 
 # Exported symbols declared in include/pt_lstm.h (tests check all are present).
 EXPORTS = ("pt_lstm_saved_bytes", "pt_lstm_workspace_bytes", "pt_lstm_forward",
-           "pt_lstm_backward", "pt_lstm_jv_penalty", "pt_lstm_last_error", "pt_lstm_version")
+           "pt_lstm_backward", "pt_lstm_jv_penalty", "pt_lstm_stem_workspace_bytes",
+           "pt_lstm_stem_forward", "pt_lstm_stem_backward", "pt_lstm_last_error",
+           "pt_lstm_version")
 
 _P = ctypes.c_void_p
 
@@ -78,6 +81,13 @@ def load():
         lib.pt_lstm_backward.argtypes = [D, _P, _P, _P, _P, ctypes.POINTER(Grads), _P]
         lib.pt_lstm_jv_penalty.restype = ctypes.c_int
         lib.pt_lstm_jv_penalty.argtypes = [D, _P, _P, ctypes.c_float, _P, _P]
+        lib.pt_lstm_stem_workspace_bytes.restype = ctypes.c_size_t
+        lib.pt_lstm_stem_workspace_bytes.argtypes = [ctypes.c_int]
+        _i, _ll = ctypes.c_int, ctypes.c_longlong
+        lib.pt_lstm_stem_forward.restype = ctypes.c_int
+        lib.pt_lstm_stem_forward.argtypes = [_P, _P, _P, _i, _i, _i, _ll, _P, _P]
+        lib.pt_lstm_stem_backward.restype = ctypes.c_int
+        lib.pt_lstm_stem_backward.argtypes = [_P, _P, _P, _P, _i, _i, _i, _ll, _P, _P, _P, _P]
         lib.pt_lstm_last_error.restype = ctypes.c_char_p
         lib.pt_lstm_version.restype = ctypes.c_char_p
         _lib = lib
@@ -215,3 +225,51 @@ def run_steps(x, weights, *, ksize: int, steps: int, h0=None, c0=None, dtype: st
               want_jv: bool = False, mu: float = 0.9):
     """Apply ``steps`` ConvLSTM steps.  ``weights``: [Wx_i..o, bx_i..o, Wh_i..o]."""
     return LSTMStepsFn.apply(x, h0, c0, ksize, steps, dtype, want_jv, mu, *weights)
+
+
+class StemFn(torch.autograd.Function):
+    """softplus(Conv3d 1x1x1) of a clip batch through pt_lstm_stem_* (HIP).
+
+    x [B,cin,T,H,W] (no gradient: it is the clip), weight [cout,cin,1,1,1],
+    bias [cout] -> [B,cout,T,H,W]; the backward returns weight / bias grads.
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _require_device(x)
+        if x.requires_grad:
+            raise NotImplementedError("the stem gives no gradient for its input")
+        lib = load()
+        b, cin = x.shape[:2]
+        cout = weight.shape[0]
+        n = x[0, 0].numel()
+        x = x.contiguous().float()
+        w = weight.detach().reshape(cout, cin).contiguous().float()
+        bb = bias.detach().contiguous().float()
+        y = torch.empty((b, cout) + tuple(x.shape[2:]), device=x.device)
+        check(lib.pt_lstm_stem_forward(_ptr(x), _ptr(w), _ptr(bb), b, cin, cout, n, _ptr(y),
+                                       _stream(x.device)))
+        ctx.save_for_backward(x, w, bb)
+        ctx.wshape = weight.shape
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        lib = load()
+        x, w, bb = ctx.saved_tensors
+        b, cin = x.shape[:2]
+        cout = w.shape[0]
+        dy = dy.contiguous().float()
+        ws = torch.empty(lib.pt_lstm_stem_workspace_bytes(cin), dtype=torch.uint8, device=x.device)
+        dw = torch.empty((cout, cin), device=x.device)
+        db = torch.empty((cout,), device=x.device)
+        check(lib.pt_lstm_stem_backward(_ptr(x), _ptr(w), _ptr(bb), _ptr(dy), b, cin, cout,
+                                        x[0, 0].numel(), _ptr(ws), _ptr(dw), _ptr(db),
+                                        _stream(x.device)))
+        return None, dw.reshape(ctx.wshape), db
+
+
+def stem(x, weight, bias):
+    """softplus(conv3d(x, weight, bias)) for a 1x1x1 ``weight`` (ConvLSTMVideo's stem)."""
+    return StemFn.apply(x, weight, bias)

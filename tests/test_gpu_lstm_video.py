@@ -86,3 +86,27 @@ def test_registry_builds_it():
     from utils import engine
     m = engine.model_selector(types.SimpleNamespace(model="convlstm"), timesteps=8, device="cpu")
     assert type(m).__name__ == "ConvLSTMVideo" and m.kernel_size == 7
+
+
+@pytest.mark.parametrize("cin,cout,b,t", [(3, 25, 3, 6), (1, 32, 2, 4), (4, 7, 5, 2)])
+def test_stem_matches_torch(cin, cout, b, t):
+    """pt_lstm_stem_* (softplus of a 1x1x1 Conv3d) against torch in f32,
+    including pre-activations past softplus's threshold (20) where it is linear."""
+    from ptamd import lstm
+    dev = _dev()
+    g = torch.Generator().manual_seed(cin * 100 + cout)
+    x = torch.rand((b, cin, t, 32, 32), generator=g).to(dev)
+    w = (torch.randn((cout, cin, 1, 1, 1), generator=g) * 4).to(dev).requires_grad_()
+    bias = torch.randn((cout,), generator=g) * 8
+    bias[0] = 21.0                                          # straddles the threshold
+    bias = bias.to(dev).requires_grad_()
+    dy = torch.randn((b, cout, t, 32, 32), generator=g).to(dev)
+    y = lstm.stem(x, w, bias)
+    (y * dy).sum().backward()
+    w2, b2 = w.detach().clone().requires_grad_(), bias.detach().clone().requires_grad_()
+    yr = F.softplus(F.conv3d(x.double(), w2.double(), b2.double()))
+    (yr * dy.double()).sum().backward()
+    assert (yr.detach() > 20).any()
+    torch.testing.assert_close(y.double(), yr.detach(), rtol=1e-5, atol=1e-5)
+    for a, r in ((w.grad, w2.grad), (bias.grad, b2.grad)):
+        assert float((a.double() - r).abs().max()) <= 1e-4 * float(r.abs().max()) + 1e-6

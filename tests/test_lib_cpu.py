@@ -184,6 +184,14 @@ def test_lstm_size_queries_and_validation():
         setattr(bad, field, val)
         assert lib.pt_lstm_saved_bytes(ctypes.byref(bad)) == 0, field
         assert msg in lib.pt_lstm_last_error(), (field, lib.pt_lstm_last_error())
+    # the clip stem validates before touching the device (dummy pointers)
+    assert lib.pt_lstm_stem_workspace_bytes(3) == 1024 * 32 * 4 * 4
+    assert lib.pt_lstm_stem_workspace_bytes(5) == 0
+    dummy = ctypes.c_void_p(16)
+    for cin, cout, n, msg in ((5, 25, 1024, b"cin 1..4"), (3, 33, 1024, b"cout 1..32"),
+                              (3, 25, 1022, b"multiple of 4")):
+        rc = lib.pt_lstm_stem_forward(dummy, dummy, dummy, 2, cin, cout, n, dummy, None)
+        assert rc == lstm.PT_LSTM_ERR_UNSUPPORTED and msg in lib.pt_lstm_last_error(), msg
 
 
 def test_convlstm_keys_and_init_match_reference():
