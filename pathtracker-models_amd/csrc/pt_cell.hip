@@ -60,7 +60,7 @@ struct CellArgs {
                   // 256 skip the conv epilogue, 512 return at entry (launch floor),
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
                   // atomics, 16 skip the 1x1 weight-gradient LDS reductions,
-                  // 32 skip slab flush; precision diagnostics (f32 path only): 2048 round
+                  // 32 skip slab flush, 16384 skip the conv weight-slice staging; precision diagnostics (f32 path only): 2048 round
                   // the stored E_t to bf16, 4096 the stored I_t, 8192 the stored gE_t, eg_t
   const void* x;                        // f32 [B][3][T][H][W] or u8 [B][T][H][W][3] (xu8)
   int xu8;
@@ -151,14 +151,14 @@ __device__ void stage_x(const void* __restrict__ xv, int xu8, f32x4* xs, int v, 
 // right) are channel chunks of the neighbouring tiles (ld maps a chunk's
 // element offset to its 16 B, e.g. applying BatchNorm backward); positions
 // outside the frame keep the zeros of tile_zero.
-template <class S, int PAD, class Ld>
+template <class S, int PAD, int NTH = NT, class Ld>
 __device__ __forceinline__ void tile_halo(S* __restrict__ tile, int v, int ntx, int nty, int pass,
                                           int tid, Ld&& ld) {
   constexpr int CPB = 16 / (int)sizeof(S);
   constexpr int NCH = Tr<S>::CP / CPB;
   constexpr int TW = tile_w<PAD>();
   constexpr int NHP = TW * TW - NPIX;                  // 420 (PAD 3) / 1092 (PAD 7)
-  constexpr int PER = (NHP * NCH + NT - 1) / NT;
+  constexpr int PER = (NHP * NCH + NTH - 1) / NTH;
   constexpr int BATCH = 6;                             // loads in flight per thread
   const TileLoc L = tile_loc(v, ntx, nty);
 #pragma unroll
@@ -168,7 +168,7 @@ __device__ __forceinline__ void tile_halo(S* __restrict__ tile, int v, int ntx, 
 #pragma unroll
     for (int kk = 0; kk < BATCH; ++kk) {
       const int k = k0 + kk;
-      const int idx = tid + k * NT;
+      const int idx = tid + k * NTH;
       const int hp = idx / NCH, q = idx - hp * NCH;
       int hy, hx;
       if (hp < PAD * TW) { hy = hp / TW - PAD; hx = hp % TW - PAD; }
@@ -228,13 +228,14 @@ __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps
 
 // Per-clip (mean, M2) of the conv outputs held in acc (PL layout, two-pass,
 // robust), accumulated into the fp64 batch sums.  red: 256 floats.
-__device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out, int lane,
+template <int RW, int NW>
+__device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out, int lane,
                                int wave, int tid) {
   const int h = lane >> 5;
   const int ch = pl_ch(pl_sum_reg(lane), h);
   f32x16 s = acc[0];
 #pragma unroll
-  for (int i = 1; i < RPW; ++i) s += acc[i];
+  for (int i = 1; i < RW; ++i) s += acc[i];
   const float ts = pl_lane_sum(s, lane);
   if (!(lane & 16)) red[wave * 32 + ch] = ts;
   __syncthreads();
@@ -243,23 +244,23 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RPW], float* red, double* out
   for (int g = 0; g < 4; ++g) {
     f32x4 m = *(const f32x4*)(red + 8 * g + 4 * h);
 #pragma unroll
-    for (int w = 1; w < NWAVE; ++w) m += *(const f32x4*)(red + w * 32 + 8 * g + 4 * h);
+    for (int w = 1; w < NW; ++w) m += *(const f32x4*)(red + w * 32 + 8 * g + 4 * h);
 #pragma unroll
     for (int j = 0; j < 4; ++j) mean[4 * g + j] = m[j] * (1.f / NPIX);
   }
   f32x16 q = zero16();
 #pragma unroll
-  for (int i = 0; i < RPW; ++i) {
+  for (int i = 0; i < RW; ++i) {
     const f32x16 d = acc[i] - mean;
     q += d * d;
   }
   const float tq = pl_lane_sum(q, lane);
-  if (!(lane & 16)) red[128 + wave * 32 + ch] = tq;
+  if (!(lane & 16)) red[NW * 32 + wave * 32 + ch] = tq;
   __syncthreads();
   if (tid < 32) {
     float sm = 0.f, v = 0.f;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) { sm += red[w * 32 + tid]; v += red[128 + w * 32 + tid]; }
+    for (int w = 0; w < NW; ++w) { sm += red[w * 32 + tid]; v += red[NW * 32 + w * 32 + tid]; }
     const double mn = (double)(sm * (1.f / NPIX));
     out += (blockIdx.x % NBNC) * 96;
     unsafeAtomicAdd(out + tid, mn);
@@ -320,8 +321,10 @@ struct StoreRow {
   }
 };
 
-template <class S, int FILL, int EPI, int PAD>
+template <class S, int FILL, int EPI, int PAD, int NTH = NT>
 __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int b) {
+  constexpr int NW = NTH / 64, RW = IMG / NW;      // waves, image rows per wave
+  static_assert(2 * NW * 32 <= CONV_MISC, "BN partial table");
   S* tile = (S*)smem;
   float* red = (float*)(smem + tile_bytes<S, PAD>());
   float* tbl = red + 128;       // FILL_BNBWD: per-channel A, Bc, Cc
@@ -346,7 +349,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       tbl[64 + tid] = -A * md + A * mdx * rstd * mean;
     }
   }
-  if constexpr (EPI != EPI_NONE) tile_zero<S, PAD>(tile, tid);
+  if constexpr (EPI != EPI_NONE) tile_zero<S, PAD, NTH>(tile, tid);
   __syncthreads();
 
   const bool tiled = a.ntx * a.nty > 1;
@@ -363,27 +366,28 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
     }
     return ov;
   };
+  auto ldc = [&](size_t e, int) { return *(const u32x4*)(a.src + e); };
+  auto ldb = [&](size_t e, int ch0) {
+    return bnbwd16(*(const u32x4*)(a.dc + e), *(const u32x4*)(a.raw + e), ch0);
+  };
   auto fill = [&](int pass) {
     if constexpr (FILL == FILL_COPY) {
       if (tiled)
-        tile_halo<S, PAD>(tile, b, a.ntx, a.nty, pass, tid,
-                          [&](size_t e, int) { return *(const u32x4*)(a.src + e); });
-      tile_fill<S, PAD>(tile, a.src + cb, pass, tid);
+        tile_halo<S, PAD, NTH>(tile, b, a.ntx, a.nty, pass, tid, ldc);
+      tile_fill<S, PAD, NTH>(tile, a.src + cb, pass, tid);
     } else if constexpr (FILL == FILL_BNBWD) {
       if (EPI != EPI_NONE && tiled)
-        tile_halo<S, PAD>(tile, b, a.ntx, a.nty, pass, tid, [&](size_t e, int ch0) {
-          return bnbwd16(*(const u32x4*)(a.dc + e), *(const u32x4*)(a.raw + e), ch0);
-        });
+        tile_halo<S, PAD, NTH>(tile, b, a.ntx, a.nty, pass, tid, ldb);
       constexpr int CPB = 16 / (int)sizeof(S);      // channels per 16-B chunk of S
       constexpr int NCH = Tr<S>::CP / CPB;
-      constexpr int PER = NPIX * NCH / NT;           // 16 chunks per thread
+      constexpr int PER = NPIX * NCH / NTH;          // 16 chunks per thread at 256 threads
       constexpr int BATCH = 4;
 #pragma unroll
       for (int k0 = 0; k0 < PER; k0 += BATCH) {
         uint4 dv[BATCH], rv[BATCH];
 #pragma unroll
         for (int k = 0; k < BATCH; ++k) {
-          const int idx = tid + (k0 + k) * NT;
+          const int idx = tid + (k0 + k) * NTH;
           const int pix = idx / NCH, q = idx % NCH;
           const size_t e = cb + (size_t)pix * C + pass * Tr<S>::CP + q * CPB;
           dv[k] = *(const uint4*)(a.dc + e);
@@ -391,7 +395,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
         }
 #pragma unroll
         for (int k = 0; k < BATCH; ++k) {
-          const int idx = tid + (k0 + k) * NT;
+          const int idx = tid + (k0 + k) * NTH;
           const int pix = idx / NCH, q = idx % NCH;
           const int ch0 = pass * Tr<S>::CP + q * CPB;
           const S* rr = (const S*)&rv[k];
@@ -418,23 +422,23 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
     for (int pass = 0; pass < Tr<S>::NPASS; ++pass) fill(pass);
     return;
   } else {
-    f32x16 acc[RPW];
+    f32x16 acc[RW];
 #pragma unroll
-    for (int i = 0; i < RPW; ++i) acc[i] = zero16();
+    for (int i = 0; i < RW; ++i) acc[i] = zero16();
     const int px = lane & 31;
     if constexpr (EPI == EPI_FWD) {
       // each finished row is stored while the later rows' MFMAs still run
       // (all 256 workgroups storing at the very end took ~6.5 us per launch)
-      const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RPW) * IMG + px) * C, h};
-      conv_run<S, PAD>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate, sr);
+      const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RW) * IMG + px) * C, h};
+      conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate, sr);
       if (a.ablate & 256) return;
-      if (!(a.ablate & 8)) bn_fwd_partial(acc, red, a.bnacc, lane, wave, tid);
+      if (!(a.ablate & 8)) bn_fwd_partial<RW, NW>(acc, red, a.bnacc, lane, wave, tid);
     } else {
-      conv_run<S, PAD>(acc, fill, a.wf, tile, wbuf, a.K, wave * RPW, lane, tid, a.ablate);
+      conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate);
       if (a.ablate & 256) return;
 #pragma unroll
-      for (int i = 0; i < RPW; ++i) {
-        const size_t po = cb + ((size_t)(wave * RPW + i) * IMG + px) * C;
+      for (int i = 0; i < RW; ++i) {
+        const size_t po = cb + ((size_t)(wave * RW + i) * IMG + px) * C;
         f32x16 v = acc[i];
         add_pl(a.add0 + po, h, v);
         if (a.add1) add_pl(a.add1 + po, h, v);
@@ -445,16 +449,20 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
   }
 }
 // Distinct kernel names per role (rocprof summaries tell them apart).
-template <class S, int PAD>
-__global__ __launch_bounds__(NT, 1) void k_conv_fwd(ConvArgs<S> a) {     // conv + BN partials
+template <class S, int PAD, int NTH = NT>
+__global__ __launch_bounds__(NTH, 1) void k_conv_fwd(ConvArgs<S> a) {     // conv + BN partials
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL_COPY, EPI_FWD, PAD>(a, smem, blockIdx.x);
+  conv_body<S, FILL_COPY, EPI_FWD, PAD, NTH>(a, smem, blockIdx.x);
 }
-template <class S, int PAD>
-__global__ __launch_bounds__(NT, 1) void k_conv_bwd(ConvArgs<S> a) {     // BN bwd + conv^T + adds
+template <class S, int PAD, int NTH = NT>
+__global__ __launch_bounds__(NTH, 1) void k_conv_bwd(ConvArgs<S> a) {     // BN bwd + conv^T + adds
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_body<S, FILL_BNBWD, EPI_ADD, PAD>(a, smem, blockIdx.x);
+  conv_body<S, FILL_BNBWD, EPI_ADD, PAD, NTH>(a, smem, blockIdx.x);
 }
+// k <= 7: 8-wave workgroups, 4 image rows per wave (2 waves per SIMD; vs 4
+// waves x 8 rows: conv_fwd 34.0 -> 33.4 us, conv_bwd of the BN1 side 42.2 ->
+// 39.1 us at B=256 bf16); k > 7: 4 waves x 8 rows (the 46 x 46 tile)
+constexpr int CONV_NT = 512;
 template <class S>
 __global__ __launch_bounds__(NT, 1) void k_bnbwd_fill(ConvArgs<S> a) {   // frame 0: BN bwd only
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2018,8 +2026,8 @@ template <class S>
 int set_lds_attrs() {
   static thread_local bool done = false;   // per host thread; cheap either way
   if (done) return 0;
-  SETLDS((k_conv_fwd<S, PADMAX>), (conv_lds_bytes<S, PADMAX>()));
-  SETLDS((k_conv_bwd<S, PADMAX>), (conv_lds_bytes<S, PADMAX>()));
+  SETLDS((k_conv_fwd<S, PADMAX, CONV_NT>), (conv_lds_bytes<S, PADMAX>()));
+  SETLDS((k_conv_bwd<S, PADMAX, CONV_NT>), (conv_lds_bytes<S, PADMAX>()));
   SETLDS((k_conv_fwd<S, PADBIG>), (conv_lds_bytes<S, PADBIG>()));
   SETLDS((k_conv_bwd<S, PADBIG>), (conv_lds_bytes<S, PADBIG>()));
   SETLDS((k_bnbwd_fill<S>), conv_lds_bytes<S>());
@@ -2049,14 +2057,14 @@ int set_lds_attrs() {
 template <class S>
 void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   if (p.K <= 2 * PADMAX + 1)
-    hipLaunchKernelGGL((k_conv_fwd<S, PADMAX>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADMAX>()), st, c);
+    hipLaunchKernelGGL((k_conv_fwd<S, PADMAX, CONV_NT>), dim3(p.B), dim3(CONV_NT), (conv_lds_bytes<S, PADMAX>()), st, c);
   else
     hipLaunchKernelGGL((k_conv_fwd<S, PADBIG>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADBIG>()), st, c);
 }
 template <class S>
 void launch_conv_bwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   if (p.K <= 2 * PADMAX + 1)
-    hipLaunchKernelGGL((k_conv_bwd<S, PADMAX>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADMAX>()), st, c);
+    hipLaunchKernelGGL((k_conv_bwd<S, PADMAX, CONV_NT>), dim3(p.B), dim3(CONV_NT), (conv_lds_bytes<S, PADMAX>()), st, c);
   else
     hipLaunchKernelGGL((k_conv_bwd<S, PADBIG>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADBIG>()), st, c);
 }

@@ -363,33 +363,33 @@ __host__ __device__ constexpr int tile_bytes() {
   return tile_w<PAD>() * tile_w<PAD>() * Tr<S>::CP * (int)sizeof(S);
 }
 
-template <class S, int PAD = PADMAX>
+template <class S, int PAD = PADMAX, int NTH = NT>
 __device__ void tile_zero(S* tile, int tid) {
   uint4* p = (uint4*)tile;
   const int n = tile_bytes<S, PAD>() / 16;
-  for (int i = tid; i < n; i += NT) p[i] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < n; i += NTH) p[i] = make_uint4(0, 0, 0, 0);
 }
 
 // Fill the tile interior with channels [pass*CP, pass*CP+CP) of a
 // channels-last clip image (global, [32][32][32] of S).  All 16 loads of a
 // thread are issued before any LDS store so one memory round trip covers the
 // whole 64 KB image (one wave per SIMD has nothing else to hide latency with).
-template <class S, int PAD = PADMAX>
+template <class S, int PAD = PADMAX, int NTH = NT>
 __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restrict__ src,
                                           int pass, int tid) {
   constexpr int CPB = 16 / (int)sizeof(S);          // channels per 16-B chunk
   constexpr int NCH = Tr<S>::CP / CPB;               // chunks per pixel
-  constexpr int PER = NPIX * NCH / NT;               // chunks per thread (16)
+  constexpr int PER = NPIX * NCH / NTH;              // chunks per thread (16 at 256 threads)
   uint4 v[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int idx = tid + k * NT;
+    const int idx = tid + k * NTH;
     const int pix = idx / NCH, q = idx % NCH;
     v[k] = *(const uint4*)(src + pix * C + pass * Tr<S>::CP + q * CPB);
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int idx = tid + k * NT;
+    const int idx = tid + k * NTH;
     const int pix = idx / NCH, q = idx % NCH;
     const int y = pix >> 5, x = pix & 31;
     *(uint4*)(tile + tile_off<S, PAD>(y + PAD, x + PAD, q * CPB)) = v[k];
@@ -412,7 +412,7 @@ constexpr int CONV_PF = 3;          // A-fragment prefetch depth (tile rows)
 constexpr int WSLICE_CHUNKS = 896;   // 16-B chunks per slice: 7 taps x 2 x 64 x 16 B (bf16)
                                      //                       = 7 taps x 8 x 64 x 4 B (f32, per pass)
 constexpr int WSLICE_BYTES = WSLICE_CHUNKS * 16;
-constexpr int WSLICE_PER = (WSLICE_CHUNKS + NT - 1) / NT;   // chunks per thread (4)
+template <int NTH> constexpr int wslice_per() { return (WSLICE_CHUNKS + NTH - 1) / NTH; }  // 4 / 2
 
 // A slice in flight: four named chunks (an array here ends up in scratch).
 struct WSlice { u32x4 v0, v1, v2, v3; };
@@ -422,9 +422,9 @@ template <int J> __device__ __forceinline__ u32x4& wsl(WSlice& w) {
   else if constexpr (J == 2) return w.v2;
   else return w.v3;
 }
-static_assert(WSLICE_PER == 4, "WSlice holds 4 chunks per thread");
+static_assert(wslice_per<NT>() == 4, "WSlice holds 4 chunks per thread");
 
-template <class S, int K, int J>
+template <class S, int K, int J, int NTH>
 __device__ __forceinline__ void wslice_load1(WSlice& r, const typename Tr<S>::frag* __restrict__ wf,
                                              int pass, int kw, int tid) {
   using TT = Tr<S>;
@@ -432,26 +432,29 @@ __device__ __forceinline__ void wslice_load1(WSlice& r, const typename Tr<S>::fr
   constexpr int RC = 64 * (int)sizeof(typename TT::frag) / 16;   // chunks per (tap, k-step) row
   constexpr int N = K * KSP * RC;
   // unconditional (clamped) loads: predicated ones get parked in scratch
-  const int e = tid + J * NT < N ? tid + J * NT : N - 1;
+  const int e = tid + J * NTH < N ? tid + J * NTH : N - 1;
   const int kh = e / (KSP * RC), rem = e - kh * (KSP * RC);
   const int s = rem / RC, q = rem - s * RC;
   wsl<J>(r) = ((const u32x4*)(wf + ((kh * K + kw) * TT::KS + pass * KSP + s) * 64))[q];
 }
-template <class S, int K>
+template <class S, int K, int NTH = NT>
 __device__ __forceinline__ void wslice_load(WSlice& r, const typename Tr<S>::frag* __restrict__ wf,
                                             int pass, int kw, int tid) {
-  wslice_load1<S, K, 0>(r, wf, pass, kw, tid);
-  wslice_load1<S, K, 1>(r, wf, pass, kw, tid);
-  wslice_load1<S, K, 2>(r, wf, pass, kw, tid);
-  wslice_load1<S, K, 3>(r, wf, pass, kw, tid);
+  constexpr int PER = wslice_per<NTH>();
+  wslice_load1<S, K, 0, NTH>(r, wf, pass, kw, tid);
+  if constexpr (PER > 1) wslice_load1<S, K, 1, NTH>(r, wf, pass, kw, tid);
+  if constexpr (PER > 2) wslice_load1<S, K, 2, NTH>(r, wf, pass, kw, tid);
+  if constexpr (PER > 3) wslice_load1<S, K, 3, NTH>(r, wf, pass, kw, tid);
 }
-template <int K>
+template <int K, int NTH = NT>
 __device__ __forceinline__ void wslice_store(WSlice& r, char* buf, int tid) {
+  constexpr int PER = wslice_per<NTH>();
+  static_assert(PER <= 4, "WSlice holds at most 4 chunks per thread");
   u32x4* b = (u32x4*)buf;
-  b[tid] = r.v0;
-  b[tid + NT] = r.v1;
-  b[tid + 2 * NT] = r.v2;
-  if (tid + 3 * NT < WSLICE_CHUNKS) b[tid + 3 * NT] = r.v3;
+  if (PER > 1 || tid < WSLICE_CHUNKS) b[tid] = r.v0;
+  if constexpr (PER > 1) { if (PER > 2 || tid + NTH < WSLICE_CHUNKS) b[tid + NTH] = r.v1; }
+  if constexpr (PER > 2) { if (PER > 3 || tid + 2 * NTH < WSLICE_CHUNKS) b[tid + 2 * NTH] = r.v2; }
+  if constexpr (PER > 3) { if (tid + 3 * NTH < WSLICE_CHUNKS) b[tid + 3 * NTH] = r.v3; }
 }
 
 // Row-final hook: called as done(i, acc[i]) the moment output row i has
@@ -465,8 +468,8 @@ struct NoRowHook {
 // k > 7 (PAD = PADBIG): the 46 x 46 tile leaves no LDS for weight slices;
 // every wave reads its column's K x KSP B fragments straight from L2 at the
 // top of the column (the ~K * RPW * KSP MFMAs of the column cover the fetch).
-template <class S, int K, int PAD, class Fill, class Done = NoRowHook>
-__device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
+template <class S, int K, int PAD, int RW, int NTH, class Fill, class Done = NoRowHook>
+__device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
                                            const typename Tr<S>::frag* __restrict__ wf, S* tile,
                                            char* wbuf, int row0, int lane, int tid, int ablate,
                                            const Done& done = Done()) {
@@ -475,21 +478,21 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
   constexpr bool LDSW = K <= 2 * PADMAX + 1;  // weight slices staged in LDS
   constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
   constexpr int off = PAD - K / 2;
-  constexpr int NTR = RPW + K - 1;          // tile rows touched by this wave
+  constexpr int NTR = RW + K - 1;           // tile rows touched by this wave
   const int h = lane >> 5, px = lane & 31;
   for (int pass = 0; pass < TT::NPASS; ++pass) {
     WSlice pre;
-    if constexpr (LDSW) wslice_load<S, K>(pre, wf, pass, 0, tid);
+    if constexpr (LDSW) wslice_load<S, K, NTH>(pre, wf, pass, 0, tid);
     __syncthreads();
     if (!(ablate & 2)) fill(pass);
-    if constexpr (LDSW) wslice_store<K>(pre, wbuf, tid);
+    if constexpr (LDSW) wslice_store<K, NTH>(pre, wbuf, tid);
     __syncthreads();
     if (ablate & 1) continue;
     for (int kw = 0; kw < K; ++kw) {
       F bc[K][KSP];
       if constexpr (LDSW) {
         const F* wl = (const F*)(wbuf + (kw & 1) * WSLICE_BYTES) + lane;
-        if (kw + 1 < K) wslice_load<S, K>(pre, wf, pass, kw + 1, tid);
+        if (kw + 1 < K && !(ablate & 16384)) wslice_load<S, K, NTH>(pre, wf, pass, kw + 1, tid);
 #pragma unroll
         for (int kh = 0; kh < K; ++kh)
 #pragma unroll
@@ -529,18 +532,18 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
 #pragma unroll
           for (int kh = 0; kh < K; ++kh) {
             const int i = tr - kh;
-            if (i >= 0 && i < RPW) acc[i] = TT::mma(bc[kh][s], av[tr][s], acc[i]);
+            if (i >= 0 && i < RW) acc[i] = TT::mma(bc[kh][s], av[tr][s], acc[i]);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (Done::active) {
           const int i = tr - (K - 1);
-          if (i >= 0 && i < RPW && kw == K - 1 && pass == TT::NPASS - 1) done(i, acc[i < 0 ? 0 : i]);
+          if (i >= 0 && i < RW && kw == K - 1 && pass == TT::NPASS - 1) done(i, acc[i < 0 ? 0 : i]);
         }
       }
       if constexpr (LDSW) {
-        if (kw + 1 < K) {
-          wslice_store<K>(pre, wbuf + ((kw + 1) & 1) * WSLICE_BYTES, tid);
+        if (kw + 1 < K && !(ablate & 16384)) {
+          wslice_store<K, NTH>(pre, wbuf + ((kw + 1) & 1) * WSLICE_BYTES, tid);
           __syncthreads();
         }
       }
@@ -548,24 +551,24 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RPW], Fill& fill,
   }
 }
 
-template <class S, int PAD, class Fill, class Done = NoRowHook>
-__device__ __forceinline__ void conv_run(f32x16 (&acc)[RPW], Fill& fill,
+template <class S, int PAD, int RW = RPW, int NTH = NT, class Fill, class Done = NoRowHook>
+__device__ __forceinline__ void conv_run(f32x16 (&acc)[RW], Fill& fill,
                                          const typename Tr<S>::frag* __restrict__ wf, S* tile,
                                          char* wbuf, int K, int row0, int lane, int tid,
                                          int ablate, const Done& done = Done()) {
   if constexpr (PAD == PADMAX) {
     switch (K) {
-      case 7: conv_run_k<S, 7, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-      case 5: conv_run_k<S, 5, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-      case 3: conv_run_k<S, 3, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-      default: conv_run_k<S, 1, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 7: conv_run_k<S, 7, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 5: conv_run_k<S, 5, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 3: conv_run_k<S, 3, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      default: conv_run_k<S, 1, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
     }
   } else {
     switch (K) {
-      case 15: conv_run_k<S, 15, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-      case 13: conv_run_k<S, 13, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-      case 11: conv_run_k<S, 11, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
-      default: conv_run_k<S, 9, PAD>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 15: conv_run_k<S, 15, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 13: conv_run_k<S, 13, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      case 11: conv_run_k<S, 11, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
+      default: conv_run_k<S, 9, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
     }
   }
 }

@@ -11,5 +11,5 @@ for ctrs in "SQ_WAVES SQ_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_A
   timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d gpurun_out/pmcpw$i -o run -- python3 tools/pmc_cell.py > gpurun_out/pmcpw$i.log 2>&1
   r=$?; echo PASS$i $r; [ $r -eq 0 ] || { tail -5 gpurun_out/pmcpw$i.log; exit $r; }
 done
-python tools/pmc_summary.py gpurun_out/pmcpw1 gpurun_out/pmcpw2 gpurun_out/pmcpw3 > gpurun_out/pmcpw_summary.txt
+python tools/pmc_summary.py gpurun_out/pmcpw_summary.json gpurun_out/pmcpw1 gpurun_out/pmcpw2 gpurun_out/pmcpw3 > gpurun_out/pmcpw_summary.txt
 cat gpurun_out/pmcpw_summary.txt
