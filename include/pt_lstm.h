@@ -96,17 +96,20 @@ int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace
 
 /* Frame stem of the clip ConvLSTM (the stem of InT.py:192,212-213
  * applied per frame): y = softplus(W x + b), a 1x1x1 channel mix over the n
- * voxels of x [B,cin,n] into y [B,cout,n] (n = T*H*W, a multiple of 4; cin
+ * voxels of the clip batch into y [B,cout,n] (n = T*H*W, a multiple of 4; cin
  * 1..4, cout 1..32; softplus as torch's F.softplus, beta 1, threshold 20).
+ * x is the f32 model input [B,cin,n] (x_u8 = 0) or the raw clip bytes u8
+ * [B,n,cin] as the TFRecords hold them (x_u8 = 1, [B,T,H,W,3]; converted
+ * as engine.prepare_data does, u / 255 in float64 rounded to f32).
  * The backward recomputes W x + b and writes dW [cout,cin] and db [cout]
  * (either may be NULL) through a workspace of pt_lstm_stem_workspace_bytes(cin)
- * bytes; the stem input x never needs a gradient (it is the clip). */
+ * bytes; the stem input never needs a gradient (it is the clip). */
 size_t pt_lstm_stem_workspace_bytes(int cin);
-int pt_lstm_stem_forward(const float* x, const float* w, const float* b, int B, int cin, int cout,
-                         long long n, float* y, pt_lstm_stream_t stream);
-int pt_lstm_stem_backward(const float* x, const float* w, const float* b, const float* dy, int B,
-                          int cin, int cout, long long n, void* workspace, float* dw, float* db,
-                          pt_lstm_stream_t stream);
+int pt_lstm_stem_forward(const void* x, int x_u8, const float* w, const float* b, int B, int cin,
+                         int cout, long long n, float* y, pt_lstm_stream_t stream);
+int pt_lstm_stem_backward(const void* x, int x_u8, const float* w, const float* b, const float* dy,
+                          int B, int cin, int cout, long long n, void* workspace, float* dw,
+                          float* db, pt_lstm_stream_t stream);
 
 const char* pt_lstm_last_error(void);
 const char* pt_lstm_version(void);

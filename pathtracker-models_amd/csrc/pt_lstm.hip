@@ -641,15 +641,40 @@ __device__ __forceinline__ float dsoftplus20(float z, float g) {
   return g * e / (e + 1.f);
 }
 
+// The stem input: the f32 model input [B][CIN][n] (planar), or the raw clip
+// bytes u8 [B][n][CIN] as the TFRecords hold them (voxel-interleaved),
+// converted exactly as engine.prepare_data does (utils/engine.py:220-255: the
+// float64 quotient u / 255 rounded to f32), so the f32 clip tensor never exists.
 template <int CIN>
-__global__ __launch_bounds__(256) void k_stem_fwd(const float4* __restrict__ x, const float* __restrict__ w,
+__device__ __forceinline__ void stem_load(const void* __restrict__ xv, int xu8, long bi, long v,
+                                          long n4, float4 (&xi)[CIN]) {
+  if (xu8) {
+    // 4 voxels x CIN bytes, 4-byte aligned (v counts groups of 4 voxels)
+    const uint32_t* q = (const uint32_t*)((const uint8_t*)xv + (bi * n4 + v) * 4 * CIN);
+    uint32_t wd[CIN];
+#pragma unroll
+    for (int j = 0; j < CIN; ++j) wd[j] = q[j];
+#pragma unroll
+    for (int j = 0; j < 4 * CIN; ++j) {
+      const float f = (float)((double)((wd[j >> 2] >> (8 * (j & 3))) & 0xffu) / 255.0);
+      const int vox = j / CIN, k = j % CIN;
+      if (vox == 0) xi[k].x = f; else if (vox == 1) xi[k].y = f; else if (vox == 2) xi[k].z = f; else xi[k].w = f;
+    }
+  } else {
+    const float4* x = (const float4*)xv;
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) xi[k] = x[(bi * CIN + k) * n4 + v];
+  }
+}
+
+template <int CIN>
+__global__ __launch_bounds__(256) void k_stem_fwd(const void* __restrict__ x, int xu8, const float* __restrict__ w,
                                                   const float* __restrict__ b, float4* __restrict__ y,
                                                   int cout, long n4, long total4) {
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total4; e += (long)gridDim.x * blockDim.x) {
     const long bi = e / n4, v = e - bi * n4;
     float4 xi[CIN];
-#pragma unroll
-    for (int k = 0; k < CIN; ++k) xi[k] = x[(bi * CIN + k) * n4 + v];
+    stem_load<CIN>(x, xu8, bi, v, n4, xi);
     for (int o = 0; o < cout; ++o) {
       float4 z = make_float4(b[o], b[o], b[o], b[o]);
 #pragma unroll
@@ -667,7 +692,7 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const float4* __restrict__ x, 
 // partial sums part[block][32 * (CIN + 1)] (wave shuffles, then LDS across the
 // 4 waves), summed in fixed order by k_stem_reduce (deterministic).
 template <int CIN>
-__global__ __launch_bounds__(256) void k_stem_bwd(const float4* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void k_stem_bwd(const void* __restrict__ x, int xu8, const float* __restrict__ w,
                                                   const float* __restrict__ b, const float4* __restrict__ dy,
                                                   float* __restrict__ part, int cout, long n4, long total4) {
   constexpr int NA = 32 * (CIN + 1);
@@ -677,8 +702,7 @@ __global__ __launch_bounds__(256) void k_stem_bwd(const float4* __restrict__ x, 
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total4; e += (long)gridDim.x * blockDim.x) {
     const long bi = e / n4, v = e - bi * n4;
     float4 xi[CIN];
-#pragma unroll
-    for (int k = 0; k < CIN; ++k) xi[k] = x[(bi * CIN + k) * n4 + v];
+    stem_load<CIN>(x, xu8, bi, v, n4, xi);
 #pragma unroll
     for (int o = 0; o < 32; ++o) {
       if (o < cout) {
@@ -1065,7 +1089,7 @@ int run_jv(const pt_lstm_desc* d, const char* sv, char* ws, float mu, float* jv,
 
 constexpr int STEM_BLOCKS = 1024;
 
-int stem_check(const float* x, const float* w, int B, int cin, int cout, long long n) {
+int stem_check(const void* x, const float* w, int B, int cin, int cout, long long n) {
   if (!x || !w) return fail(PT_LSTM_ERR_ARG, "null x / w%ld");
   if (B < 1 || cin < 1 || cin > 4 || cout < 1 || cout > 32)
     return fail(PT_LSTM_ERR_UNSUPPORTED, "stem needs B >= 1, cin 1..4, cout 1..32 (cin=%ld)", cin);
@@ -1141,15 +1165,16 @@ size_t pt_lstm_stem_workspace_bytes(int cin) {
   return cin < 1 || cin > 4 ? 0 : (size_t)STEM_BLOCKS * 32 * (cin + 1) * sizeof(float);
 }
 
-int pt_lstm_stem_forward(const float* x, const float* w, const float* b, int B, int cin, int cout,
-                         long long n, float* y, pt_lstm_stream_t stream) {
+int pt_lstm_stem_forward(const void* x, int x_u8, const float* w, const float* b, int B, int cin,
+                         int cout, long long n, float* y, pt_lstm_stream_t stream) {
   if (int rc = stem_check(x, w, B, cin, cout, n)) return rc;
+  if (x_u8 != 0 && x_u8 != 1) return fail(PT_LSTM_ERR_ARG, "bad x_u8 (%ld)", x_u8);
   if (!b || !y) return fail(PT_LSTM_ERR_ARG, "null b / y%ld");
   const long n4 = (long)(n / 4), total4 = (long)B * n4;
   const int grid = (int)std::min<long>((total4 + 255) / 256, 8192);
   hipStream_t st = (hipStream_t)stream;
   switch (cin) {
-#define STEM_F(C) case C: hipLaunchKernelGGL(k_stem_fwd<C>, dim3(grid), dim3(256), 0, st, (const float4*)x, w, b, (float4*)y, cout, n4, total4); break;
+#define STEM_F(C) case C: hipLaunchKernelGGL(k_stem_fwd<C>, dim3(grid), dim3(256), 0, st, x, x_u8, w, b, (float4*)y, cout, n4, total4); break;
     STEM_F(1) STEM_F(2) STEM_F(3) STEM_F(4)
 #undef STEM_F
   }
@@ -1157,16 +1182,17 @@ int pt_lstm_stem_forward(const float* x, const float* w, const float* b, int B, 
   return 0;
 }
 
-int pt_lstm_stem_backward(const float* x, const float* w, const float* b, const float* dy, int B,
-                          int cin, int cout, long long n, void* workspace, float* dw, float* db,
-                          pt_lstm_stream_t stream) {
+int pt_lstm_stem_backward(const void* x, int x_u8, const float* w, const float* b, const float* dy,
+                          int B, int cin, int cout, long long n, void* workspace, float* dw,
+                          float* db, pt_lstm_stream_t stream) {
   if (int rc = stem_check(x, w, B, cin, cout, n)) return rc;
+  if (x_u8 != 0 && x_u8 != 1) return fail(PT_LSTM_ERR_ARG, "bad x_u8 (%ld)", x_u8);
   if (!b || !dy || !workspace) return fail(PT_LSTM_ERR_ARG, "null b / dy / workspace%ld");
   const long n4 = (long)(n / 4), total4 = (long)B * n4;
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)workspace;
   switch (cin) {
-#define STEM_B(C) case C: hipLaunchKernelGGL(k_stem_bwd<C>, dim3(STEM_BLOCKS), dim3(256), 0, st, (const float4*)x, w, b, (const float4*)dy, part, cout, n4, total4); break;
+#define STEM_B(C) case C: hipLaunchKernelGGL(k_stem_bwd<C>, dim3(STEM_BLOCKS), dim3(256), 0, st, x, x_u8, w, b, (const float4*)dy, part, cout, n4, total4); break;
     STEM_B(1) STEM_B(2) STEM_B(3) STEM_B(4)
 #undef STEM_B
   }

@@ -31,6 +31,7 @@ from torch.autograd import Function
 from torch.nn import init
 
 from ptamd import lstm
+from ptamd.cell import target_channel
 from ptamd.lstm import run_steps
 
 _DEFAULT_DTYPE = os.environ.get("PT_CELL_DTYPE", "f32")
@@ -243,6 +244,10 @@ class ConvLSTMVideo(nn.Module):
     def cell_dtype(self, v):
         self.unit1.cell_dtype = v
 
+    # forward also takes the raw u8 clips [B,T,H,W,3] (engine.prepare_data
+    # keep_u8): the stem kernel converts them exactly as prepare_data would
+    accepts_u8 = True
+
     def forward(self, x, testmode=False):
         if testmode:
             raise NotImplementedError("ConvLSTMVideo has no per-frame testmode outputs")
@@ -252,7 +257,7 @@ class ConvLSTMVideo(nn.Module):
         steps = xbn.shape[2]
         want_jv = self.training and steps >= 2
         h_t, _, jv = self.unit1.steps(xbn, steps, want_jv=want_jv)
-        out = torch.cat([self.readout_conv(h_t), x[:, 2, 0][:, None]], 1)
+        out = torch.cat([self.readout_conv(h_t), target_channel(x)[:, None]], 1)
         out = self.target_conv(out)
         out = F.avg_pool2d(out, kernel_size=out.size()[2:])
         out = self.readout_dense(out.reshape(x.shape[0], -1))

@@ -85,9 +85,9 @@ def load():
         lib.pt_lstm_stem_workspace_bytes.argtypes = [ctypes.c_int]
         _i, _ll = ctypes.c_int, ctypes.c_longlong
         lib.pt_lstm_stem_forward.restype = ctypes.c_int
-        lib.pt_lstm_stem_forward.argtypes = [_P, _P, _P, _i, _i, _i, _ll, _P, _P]
+        lib.pt_lstm_stem_forward.argtypes = [_P, _i, _P, _P, _i, _i, _i, _ll, _P, _P]
         lib.pt_lstm_stem_backward.restype = ctypes.c_int
-        lib.pt_lstm_stem_backward.argtypes = [_P, _P, _P, _P, _i, _i, _i, _ll, _P, _P, _P, _P]
+        lib.pt_lstm_stem_backward.argtypes = [_P, _i, _P, _P, _P, _i, _i, _i, _ll, _P, _P, _P, _P]
         lib.pt_lstm_last_error.restype = ctypes.c_char_p
         lib.pt_lstm_version.restype = ctypes.c_char_p
         _lib = lib
@@ -230,8 +230,10 @@ def run_steps(x, weights, *, ksize: int, steps: int, h0=None, c0=None, dtype: st
 class StemFn(torch.autograd.Function):
     """softplus(Conv3d 1x1x1) of a clip batch through pt_lstm_stem_* (HIP).
 
-    x [B,cin,T,H,W] (no gradient: it is the clip), weight [cout,cin,1,1,1],
-    bias [cout] -> [B,cout,T,H,W]; the backward returns weight / bias grads.
+    x: the f32 model input [B,cin,T,H,W] or the raw u8 clips [B,T,H,W,cin]
+    (converted in the kernel as engine.prepare_data would; no gradient: it is
+    the clip), weight [cout,cin,1,1,1], bias [cout] -> [B,cout,T,H,W]; the
+    backward returns weight / bias grads.
     """
 
     @staticmethod
@@ -240,16 +242,22 @@ class StemFn(torch.autograd.Function):
         if x.requires_grad:
             raise NotImplementedError("the stem gives no gradient for its input")
         lib = load()
-        b, cin = x.shape[:2]
+        u8 = x.dtype == torch.uint8
+        if u8:
+            b, cin, dims = x.shape[0], x.shape[-1], tuple(x.shape[1:4])
+            x = x.contiguous()
+        else:
+            b, cin, dims = x.shape[0], x.shape[1], tuple(x.shape[2:])
+            x = x.contiguous().float()
+        n = dims[0] * dims[1] * dims[2]
         cout = weight.shape[0]
-        n = x[0, 0].numel()
-        x = x.contiguous().float()
         w = weight.detach().reshape(cout, cin).contiguous().float()
         bb = bias.detach().contiguous().float()
-        y = torch.empty((b, cout) + tuple(x.shape[2:]), device=x.device)
-        check(lib.pt_lstm_stem_forward(_ptr(x), _ptr(w), _ptr(bb), b, cin, cout, n, _ptr(y),
-                                       _stream(x.device)))
+        y = torch.empty((b, cout) + dims, device=x.device)
+        check(lib.pt_lstm_stem_forward(_ptr(x), int(u8), _ptr(w), _ptr(bb), b, cin, cout, n,
+                                       _ptr(y), _stream(x.device)))
         ctx.save_for_backward(x, w, bb)
+        ctx.meta = (int(u8), b, cin, n)
         ctx.wshape = weight.shape
         return y
 
@@ -258,15 +266,14 @@ class StemFn(torch.autograd.Function):
     def backward(ctx, dy):
         lib = load()
         x, w, bb = ctx.saved_tensors
-        b, cin = x.shape[:2]
+        u8, b, cin, n = ctx.meta
         cout = w.shape[0]
         dy = dy.contiguous().float()
         ws = torch.empty(lib.pt_lstm_stem_workspace_bytes(cin), dtype=torch.uint8, device=x.device)
         dw = torch.empty((cout, cin), device=x.device)
         db = torch.empty((cout,), device=x.device)
-        check(lib.pt_lstm_stem_backward(_ptr(x), _ptr(w), _ptr(bb), _ptr(dy), b, cin, cout,
-                                        x[0, 0].numel(), _ptr(ws), _ptr(dw), _ptr(db),
-                                        _stream(x.device)))
+        check(lib.pt_lstm_stem_backward(_ptr(x), u8, _ptr(w), _ptr(bb), _ptr(dy), b, cin, cout,
+                                        n, _ptr(ws), _ptr(dw), _ptr(db), _stream(x.device)))
         return None, dw.reshape(ctx.wshape), db
 
 

@@ -110,3 +110,29 @@ def test_stem_matches_torch(cin, cout, b, t):
     torch.testing.assert_close(y.double(), yr.detach(), rtol=1e-5, atol=1e-5)
     for a, r in ((w.grad, w2.grad), (bias.grad, b2.grad)):
         assert float((a.double() - r).abs().max()) <= 1e-4 * float(r.abs().max()) + 1e-6
+
+
+def test_u8_clips_match_f32_input():
+    """Raw u8 clips [B,T,H,W,3] through the stem kernel give the same model
+    outputs, bit for bit, as engine.prepare_data's f32 input, and the same
+    gradients (to 1e-5: MIOpen's readout weight gradient is not bitwise
+    reproducible between two identical calls)."""
+    from ptamd import synth
+    from ptamd.cell import unit_values
+    dev = _dev()
+    clips, labels = synth.make_batch(77, 3, 6)
+    xu8 = torch.from_numpy(clips).to(dev)                       # [B,T,H,W,3]
+    x32 = unit_values(xu8).permute(0, 4, 1, 2, 3).contiguous()  # [B,3,T,H,W]
+    y = torch.tensor([ord(v) for v in labels], dtype=torch.float32, device=dev).reshape(-1, 1)
+    m = _model(7, 11).to(dev).train()
+    res = []
+    for x in (x32, xu8):
+        m.zero_grad(set_to_none=True)
+        out, jv = m(x)
+        F.binary_cross_entropy_with_logits(out, y).backward()
+        res.append((out.detach().clone(), jv.clone(),
+                    {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    (o1, j1, g1), (o2, j2, g2) = res
+    assert torch.equal(o1, o2) and torch.equal(j1, j2)
+    for n in g1:
+        torch.testing.assert_close(g2[n], g1[n], rtol=1e-5, atol=1e-8, msg=n)

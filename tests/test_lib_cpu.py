@@ -190,7 +190,7 @@ def test_lstm_size_queries_and_validation():
     dummy = ctypes.c_void_p(16)
     for cin, cout, n, msg in ((5, 25, 1024, b"cin 1..4"), (3, 33, 1024, b"cout 1..32"),
                               (3, 25, 1022, b"multiple of 4")):
-        rc = lib.pt_lstm_stem_forward(dummy, dummy, dummy, 2, cin, cout, n, dummy, None)
+        rc = lib.pt_lstm_stem_forward(dummy, 0, dummy, dummy, 2, cin, cout, n, dummy, None)
         assert rc == lstm.PT_LSTM_ERR_UNSUPPORTED and msg in lib.pt_lstm_last_error(), msg
 
 

@@ -101,6 +101,8 @@ def main_video(args):
     opt = torch.optim.Adam(m.parameters(), lr=3e-4)
     crit = torch.nn.BCEWithLogitsLoss()
     x, y = make_clips(args.batch, args.frames, seed=1000)
+    if args.input == "u8":       # the same clips as raw bytes [B,T,H,W,3]
+        x = (x * 255.0).round().to(torch.uint8).permute(0, 2, 3, 4, 1).contiguous()
     x, y = x.to(dev), y.to(dev).reshape(-1, 1)
 
     def step():
@@ -126,7 +128,7 @@ def main_video(args):
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True, "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": f"ConvLSTMVideo 32x32x{args.frames}f k={args.filt} 25ch, "
-                                   f"{args.batch} clips/GPU, {args.dtype} cell"},
+                                   f"{args.batch} clips/GPU, {args.dtype} cell, {args.input} input"},
             "step_tflops": round(fl / 1e12, 2),
             "step_frac_of_mfma_peak": round(fl / 1e12 / PEAK_TFLOPS[args.dtype], 4),
             "loss": round(float(loss.item()), 5)}
@@ -185,6 +187,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--video", action="store_true", help="cfg3 on the 32x32x64f clips")
     ap.add_argument("--frames", type=int, default=64)
+    ap.add_argument("--input", default="f32", choices=["f32", "u8"],
+                    help="--video: the f32 model input, or the raw u8 clips the TFRecords hold")
     args = ap.parse_args()
     if args.video:
         if args.filt == 15 and "--filt" not in sys.argv:
