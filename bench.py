@@ -89,15 +89,18 @@ def algorithmic_bytes(kind, batch, frames, elt, xb=4):
     """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
     (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
     XF = one clip-frame of the input (3x32x32; xb = 4 B f32, 1 B raw u8 clips).
+    The excitation E is f32 in both cell dtypes: the two E
+    tensors k_pw_fa and k_pw_ba move per frame count at 4 B per element (dE).
     Implementation overhead (the per-workgroup gradient partials, BatchNorm
     sums) is not algorithmic and is not counted."""
     F, XF = C * HW * HW * elt, 3 * HW * HW * xb
+    dE = C * HW * HW * (4 - elt)
     per_clip = {
-        "k_pw_fa": frames * (XF + 7 * F),
+        "k_pw_fa": frames * (XF + 7 * F + 2 * dE),
         "k_conv_fa": frames * 2 * F,
         "k_pw_fb": frames * (XF + 3 * F),
         "k_conv_fb": frames * 2 * F,
-        "k_pw_ba": frames * (XF + 11 * F),
+        "k_pw_ba": frames * (XF + 11 * F + 2 * dE),
         "k_conv_ba": (frames - 1) * 5 * F + 3 * F,
         "k_pw_bb": frames * (XF + 8 * F),
         "k_conv_bb": frames * 6 * F,

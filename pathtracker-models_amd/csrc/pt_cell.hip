@@ -60,7 +60,9 @@ struct CellArgs {
                   // 256 skip the conv epilogue, 512 return at entry (launch floor),
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
                   // atomics, 16 skip the 1x1 weight-gradient LDS reductions,
-                  // 32 skip slab flush, 16384 skip the conv weight-slice staging; precision diagnostics (f32 path only): 2048 round
+                  // 32 skip slab flush, 16384 skip the conv weight-slice staging,
+                  // 32768 skip only the conv's BN fp64 atomics, 65536 / 131072
+                  // skip k_pw_fa's BN1 finalisation / x staging; precision diagnostics (f32 path only): 2048 round
                   // the stored E_t to bf16, 4096 the stored I_t, 8192 the stored gE_t, eg_t
   const void* x;                        // f32 [B][3][T][H][W] or u8 [B][T][H][W][3] (xu8)
   int xu8;
@@ -230,7 +232,7 @@ __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps
 // robust), accumulated into the fp64 batch sums.  red: 256 floats.
 template <int RW, int NW>
 __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out, int lane,
-                               int wave, int tid) {
+                               int wave, int tid, int ablate) {
   const int h = lane >> 5;
   const int ch = pl_ch(pl_sum_reg(lane), h);
   f32x16 s = acc[0];
@@ -257,7 +259,7 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out,
   const float tq = pl_lane_sum(q, lane);
   if (!(lane & 16)) red[NW * 32 + wave * 32 + ch] = tq;
   __syncthreads();
-  if (tid < 32) {
+  if (tid < 32 && !(ablate & 32768)) {
     float sm = 0.f, v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) { sm += red[w * 32 + tid]; v += red[NW * 32 + w * 32 + tid]; }
@@ -432,7 +434,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RW) * IMG + px) * C, h};
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate, sr);
       if (a.ablate & 256) return;
-      if (!(a.ablate & 8)) bn_fwd_partial<RW, NW>(acc, red, a.bnacc, lane, wave, tid);
+      if (!(a.ablate & 8)) bn_fwd_partial<RW, NW>(acc, red, a.bnacc, lane, wave, tid, a.ablate);
     } else {
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate);
       if (a.ablate & 256) return;
@@ -794,8 +796,8 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   const size_t ro = clip_off(b) + (size_t)y * IMG * C;
   // this wave's row tiles first: their latency overlaps the staging below
   const FaIn<S> in = fa_load(a, ro, c, h);
-  if (t < T) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
-  if (t > 0)
+  if (t < T && !(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
+  if (t > 0 && !(a.ablate & 65536))
     bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
   __syncthreads();
