@@ -1087,7 +1087,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   // one row per wave: its tiles are loaded first, their latency overlaps the staging
   BbRow<S> pre;
   if constexpr (RPP == 1) pre = load_row(clip_off(b) + (size_t)(y0 + wave) * IMG * C);
-  slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);        // i_w, i_u, e_w, e_u
+  if (!(a.ablate & 262144)) slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);   // i_w, i_u, e_w, e_u
   stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   if constexpr (!BF) gacc_zero(L.gacc, 4, tid);
   __syncthreads();

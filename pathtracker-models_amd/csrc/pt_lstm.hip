@@ -403,7 +403,12 @@ __global__ __launch_bounds__(NT, 1) void k_lwgrad(LWgradArgs a) {
   S* buf = (S*)smem;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int g = __builtin_amdgcn_readfirstlane(tid >> 6);     // gate of this wave
-  const int kh = blockIdx.x, sl = blockIdx.y;
+  // XCD-aware (kh, slice) of this workgroup: blocks b and b + 8 share an XCD
+  // (MI355X_MICROARCH.md), so the K kernel-row workgroups of one slice, which
+  // stream the same D / X bands, are dealt to the same XCD's L2
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int kh = j % K, sl = xcd + 8 * (j / K);
+  if (sl >= a.nsl) return;
   const int nimg = a.n0 + a.n1;
   const int nmine = nimg > sl ? (nimg - sl + a.nsl - 1) / a.nsl : 0;
   const int nunits = nmine * NBW;
@@ -804,6 +809,7 @@ int check(const pt_lstm_desc* d) {
 
 int slices(int nimg, int K) {
   int n = (512 + K - 1) / K;           // ~512 workgroups over the K tap rows
+  if (n >= 8) n = n / 8 * 8;           // whole XCD groups (k_lwgrad's block mapping)
   if (n > nimg) n = nimg;
   return n < 1 ? 1 : n;
 }
@@ -890,7 +896,7 @@ int conv_k(int K, const void* src, const void* wf, float* out, const float* add,
 template <class S, int K>
 int wgrad(const LWgradArgs& a, hipStream_t st) {
   using Bd = LWBand<S, K>;
-  hipLaunchKernelGGL((k_lwgrad<S, K>), dim3(K, a.nsl), dim3(NT), Bd::BYTES, st, a);
+  hipLaunchKernelGGL((k_lwgrad<S, K>), dim3(K * ((a.nsl + 7) / 8) * 8), dim3(NT), Bd::BYTES, st, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
