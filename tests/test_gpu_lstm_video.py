@@ -136,3 +136,48 @@ def test_u8_clips_match_f32_input():
     assert torch.equal(o1, o2) and torch.equal(j1, j2)
     for n in g1:
         torch.testing.assert_close(g2[n], g1[n], rtol=1e-5, atol=1e-8, msg=n)
+
+
+def test_bf16_matches_f32_at_cfg3_size():
+    """The clip ConvLSTM at its bench size (B=256, T=64, k=7): the bf16 cell
+    against the f32 cell (itself pinned to the oracle above) on the bench's
+    clips — logits within 5e-2, identical 0.5 / 0 decisions for every clip
+    farther than that from the threshold, per-tensor gradient cosine >= 0.99."""
+    import json
+    import os
+    from models import convlstm
+    dev = _dev()
+    x, y = _clips(1000, 256, 64)
+    x, y = x.to(dev), y.to(dev).reshape(-1, 1)
+    torch.manual_seed(1234)
+    m = convlstm.ConvLSTMVideo(dimensions=25, timesteps=64, kernel_size=7).to(dev).train()
+    with torch.no_grad():                                   # off the near-constant init
+        m.readout_conv.weight.mul_(8.0)
+    res = {}
+    for dt in ("f32", "bf16"):
+        m.cell_dtype = dt
+        m.zero_grad(set_to_none=True)
+        out, _ = m(x)
+        F.binary_cross_entropy_with_logits(out, y).backward()
+        torch.cuda.synchronize()
+        res[dt] = (out.detach().double().flatten().cpu(),
+                   {n: p.grad.detach().double().flatten().cpu() for n, p in m.named_parameters()})
+    (o32, g32), (o16, g16) = res["f32"], res["bf16"]
+    tol = 5e-2
+    err = float((o16 - o32).abs().max())
+    cos = {n: float(g16[n] @ g32[n] / (g16[n].norm() * g32[n].norm()))
+           for n in g32 if g32[n].norm() > 1e-12}
+    flips = {}
+    for name, thr in (("train_0.5", 0.5), ("eval_0", 0.0)):
+        far = (o32 - thr).abs() > tol
+        flips[name] = int(((o16 > thr) != (o32 > thr))[far].sum())
+    rec = {"logit_max_abs_err": err, "logit_spread": float(o32.max() - o32.min()),
+           "grad_cosine_min": min(cos.values()), "grad_cosine_min_tensor": min(cos, key=cos.get),
+           "flips_away_from_threshold": flips}
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    json.dump(rec, open(os.path.join(d, "convlstm_video_parity.json"), "w"), indent=1)
+    assert err <= tol, rec
+    assert flips == {"train_0.5": 0, "eval_0": 0}, rec
+    bad = {n: v for n, v in cos.items() if v < 0.99}
+    assert not bad, (bad, rec)
