@@ -208,9 +208,12 @@ __device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const St
 // Forward BN: batch mean / rstd per channel from the fp64 sums of per-clip
 // (mean_b, mean_b^2, M2_b) (Chan et al.: M2 = sum M2_b + n (sum mean_b^2 -
 // (sum mean_b)^2 / B)); all threads end with them in stat[0..63].
+// Lanes fl < 32 of ONE wave finalise (the caller picks the wave; others pass
+// fl >= 32); stat is read only after the caller's next workgroup barrier.
 __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps, float* stat,
-                                float* gstat, int tid) {
-  if (tid < 32) {
+                                float* gstat, int fl) {
+  if (fl < 32) {
+    const int tid = fl;
     double s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
     for (int k = 0; k < NBNC; ++k) {
@@ -225,7 +228,6 @@ __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps
     stat[32 + tid] = rstd;
     if (gstat) { gstat[tid] = (float)mean; gstat[32 + tid] = rstd; }
   }
-  __syncthreads();
 }
 
 // Per-clip (mean, M2) of the conv outputs held in acc (PL layout, two-pass,
@@ -794,12 +796,15 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   const int y0 = part * PW_NW;
   const int yl = wave, y = y0 + yl;
   const size_t ro = clip_off(b) + (size_t)y * IMG * C;
-  // this wave's row tiles first: their latency overlaps the staging below
+  // The BN1 finalisation is wave PW_NW-1's first work: loads complete in
+  // order per wave, so behind its own row tiles it would wait for all of them
+  // (and the barrier below for it); the other waves' row tiles go out first.
+  const bool finw = wave == PW_NW - 1;
+  if (finw && t > 0 && !(a.ablate & 65536))
+    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
+                    blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   const FaIn<S> in = fa_load(a, ro, c, h);
   if (t < T && !(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
-  if (t > 0 && !(a.ablate & 65536))
-    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
-                    blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
   fa_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, b, y, ro, in, lane);
@@ -887,6 +892,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   }
   const FbIn<S> in = fb_load<S, HG>(a, ro, c, h);
   stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
+  // (finalising first in a separate wave, as k_pw_fa does, measured no gain here)
   bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, B, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
