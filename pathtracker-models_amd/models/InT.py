@@ -102,9 +102,34 @@ class rCell(nn.Module):
                 getattr(self, name).requires_grad = False
 
     def forward(self, input_, inhibition, excitation, activ=F.softplus, testmode=False):
-        raise NotImplementedError(
-            "rCell runs fused over whole clips on the GPU; call InT.forward(x) "
-            "(the reference only ever calls rCell from InT's frame loop, models/InT.py:223-235)")
+        """One frame step (reference models/InT.py:145-179), for callers that
+        step the cell themselves.  ``InT.forward`` never calls this: its whole
+        T-frame recurrence and BPTT run fused in the HIP library.  The step is
+        the reference's own op graph (1x1 gate convs, k x k convs, batch-stat
+        BatchNorm) as device-agnostic torch ops, so it runs wherever its
+        arguments live and autograd differentiates it."""
+        if self.use_attention:
+            att_gate = torch.sigmoid(self.a_w_gate(input_) + self.a_u_gate(excitation))
+            gated_excitation = att_gate * excitation
+        else:
+            att_gate = None
+            gated_excitation = excitation
+        gated_input = input_
+        gated_inhibition = inhibition
+        if not self.no_inh:
+            inh_intx = self.bn[0](F.conv2d(gated_excitation, self.w_inh, padding=self.h_padding))
+            inhibition_hat = activ(input_ - activ(inh_intx * (self.alpha * gated_inhibition + self.mu)))
+            inh_gate = torch.sigmoid(self.i_w_gate(gated_input) + self.i_u_gate(gated_inhibition))
+            inhibition = (1 - inh_gate) * inhibition + inh_gate * inhibition_hat
+        else:
+            inhibition, gated_inhibition = gated_excitation, excitation
+        exc_gate = torch.sigmoid(self.e_w_gate(gated_inhibition) + self.e_u_gate(gated_excitation))
+        exc_intx = self.bn[1](F.conv2d(inhibition, self.w_exc, padding=self.h_padding))
+        excitation_hat = activ(exc_intx * (self.kappa * inhibition + self.gamma))
+        excitation = (1 - exc_gate) * excitation + exc_gate * excitation_hat
+        if testmode:
+            return inhibition, excitation, att_gate
+        return inhibition, excitation
 
 
 class InT(nn.Module):

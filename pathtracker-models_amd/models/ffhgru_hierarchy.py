@@ -80,10 +80,29 @@ class hConvGRUCell(nn.Module):
             self.e_u_gate.bias.data = -self.i_u_gate.bias.data
 
     def forward(self, input_, inhibition, excitation, activ=F.softplus, testmode=False):
-        raise NotImplementedError(
-            "hConvGRUCell runs fused over whole clips on the GPU; call FFhGRU.forward(x) "
-            "(the reference only calls the cell from FFhGRU's frame loop, "
-            "models/ffhgru_hierarchy.py:229-245)")
+        """One frame step (reference models/ffhgru_hierarchy.py:135-173), for
+        callers that step the cell themselves; ``FFhGRU.forward`` runs the
+        fused HIP recurrence instead and never calls this.  Device-agnostic
+        torch ops (the reference's op graph), differentiable by autograd.  The
+        gated inhibition is the attention map itself (:147)."""
+        if not self.use_attention:
+            raise ValueError("hConvGRUCell.forward needs use_attention=True (the reference "
+                             "leaves the gated tensors undefined otherwise, :141-148)")
+        att_gate = torch.sigmoid(self.a_w_gate(input_) + self.a_u_gate(excitation))
+        gated_input = input_
+        gated_excitation = att_gate * excitation
+        gated_inhibition = att_gate
+        inh_intx = self.bn[0](F.conv2d(gated_excitation, self.w_inh, padding=self.h_padding))
+        inhibition_hat = activ(input_ - activ(inh_intx * (self.alpha * gated_inhibition + self.mu)))
+        inh_gate = torch.sigmoid(self.i_w_gate(gated_input) + self.i_u_gate(gated_inhibition))
+        inhibition = (1 - inh_gate) * inhibition + inh_gate * inhibition_hat
+        exc_gate = torch.sigmoid(self.e_w_gate(gated_inhibition) + self.e_u_gate(gated_excitation))
+        exc_intx = self.bn[1](F.conv2d(inhibition, self.w_exc, padding=self.h_padding))
+        excitation_hat = activ(exc_intx * (self.kappa * inhibition + self.gamma))
+        excitation = (1 - exc_gate) * excitation + exc_gate * excitation_hat
+        if testmode:
+            return inhibition, excitation, att_gate
+        return inhibition, excitation
 
 
 class FFhGRU(nn.Module):

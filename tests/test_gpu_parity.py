@@ -170,3 +170,27 @@ def test_oracle_agrees_on_device_sized_batch():
     for k, p in m.named_parameters():
         if p.grad is not None:
             _assert_close(f"grad {k}", p.grad.cpu(), sd[k].grad, 1e-6, 1e-3)
+
+
+@pytest.mark.parametrize("tag", ["int_c32", "hgru_c32"])
+def test_step_api_on_gpu_matches_fused_cell(tag):
+    """The per-step cell API (rCell / hConvGRUCell.forward, torch ops on the
+    device) stepped over the clip agrees with the fused HIP recurrence."""
+    dev = _dev()
+    g = load(tag)
+    m = _model(g).to(dev)
+    x, _ = prepared_input(g)
+    x = x.to(dev)
+    with torch.no_grad():
+        fused, fstates, fgates = m(x, testmode=True)
+        xbn = m.nl(m.preproc(x))
+        b, c, t_len, h, w = xbn.shape
+        inh = torch.zeros((b, c, h, w), device=dev)
+        exc = torch.zeros((b, c, h, w), device=dev)
+        states = []
+        for t in range(t_len):
+            inh, exc, att = m.unit1(xbn[:, :, t], inh, exc, activ=m.nl, testmode=True)
+            states.append(m.readout_conv(exc))
+        stepped = m.readout(exc, x)
+    _assert_close("logits", stepped.cpu(), fused.cpu(), 1e-3)
+    _assert_close("states", torch.stack(states, 1).cpu(), fstates.cpu(), 1e-3)

@@ -2,7 +2,9 @@
 """Kernel-phase ablation timing (timing experiments only; outputs are garbage
 under ablation).  PT_CELL_ABLATE bits: 1 skip conv MFMA loop, 2 skip conv tile
 fill, 4 skip per-row element-wise loops.  Masks are interleaved in one process
-(cdna_hip_programming.md §5.4 rule 24)."""
+(cdna_hip_programming.md §5.4 rule 24).  A mask may carry variant switches,
+e.g. MASKS="0:PT_CELL_BB_RPP=1,0:PT_CELL_BB_RPP=8" (env NAME=VALUE pairs after
+':' separated by '+'), interleaved the same way."""
 import os
 import sys
 
@@ -19,7 +21,7 @@ def main():
     b = int(os.environ.get("B", 256))
     t = int(os.environ.get("T", 64))
     dtype = os.environ.get("DT", "bf16")
-    masks = [int(m) for m in os.environ.get("MASKS", "0,1,2,3,4,7").split(",")]
+    masks = os.environ.get("MASKS", "0,1,2,3,4,7").split(",")
     rounds = int(os.environ.get("ROUNDS", 3))
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -31,7 +33,10 @@ def main():
     res = {mk: {k: [] for k in kinds} for mk in masks}
     for r in range(rounds + 1):
         for mk in masks:
-            os.environ["PT_CELL_ABLATE"] = str(mk)
+            bits, _, env = mk.partition(":")
+            os.environ["PT_CELL_ABLATE"] = bits
+            extra = dict(kv.split("=", 1) for kv in env.split("+") if kv)
+            os.environ.update(extra)
             torch.cuda.synchronize()
             lib.pt_cell_timing_reset()
             lib.pt_cell_timing_enable((1 << _lib.NKINDS) - 1)
@@ -39,6 +44,8 @@ def main():
             out.sum().backward()
             torch.cuda.synchronize()
             lib.pt_cell_timing_enable(0)
+            for k in extra:
+                os.environ.pop(k)
             if r == 0:
                 continue
             for name in kinds:
@@ -53,7 +60,7 @@ def main():
         for k in kinds:
             v = sorted(res[mk][k])
             row.append(f"{v[len(v) // 2]:8.1f}" if v else " " * 8)
-        print(f"{mk:4d}  " + "  ".join(row))
+        print(f"{mk:>4}  " + "  ".join(row))
 
 
 if __name__ == "__main__":
