@@ -194,14 +194,24 @@ __device__ __forceinline__ void tile_halo(S* __restrict__ tile, int v, int ntx, 
 
 // Stem (models/InT.py:212-213): z = W_pre x + b; xbn = nl(z); CL layout.
 struct Stem { float w0, w1, w2, b; };
-template <int ACT>
+// WANT_D: z returns nl'(z) instead of z (the backward's stem gradient needs
+// only that; f and f' then share one exponential).
+template <int ACT, bool WANT_D = false>
 __device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const Stem& st,
                                         f32x16& z, f32x16& xv) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const f32x4 v = xs[yl * IMG + cl_x(r, h)];
-    z[r] = st.w0 * v[0] + st.w1 * v[1] + st.w2 * v[2] + st.b;
-    xv[r] = Act<ACT>::f(z[r]);
+    const float zr = st.w0 * v[0] + st.w1 * v[1] + st.w2 * v[2] + st.b;
+    if constexpr (WANT_D) {
+      float f, d;
+      Act<ACT>::fd(zr, f, d);
+      xv[r] = f;
+      z[r] = d;
+    } else {
+      z[r] = zr;
+      xv[r] = Act<ACT>::f(zr);
+    }
   }
 }
 
@@ -577,19 +587,27 @@ __device__ __forceinline__ void stage_wg(bf16x8* stage, int slot, const V& v, in
 }
 __device__ __forceinline__ void gate_wgrad(const bf16x8* stage, int dslot, int xslot, int g,
                                            const float* slabl, float* slab_p, int lane) {
+  // operands read one k-step ahead of their MFMA (a dependent LDS read per
+  // MFMA exposed the LDS latency 8 times)
+  constexpr int NK = PW_NW * 2;
+  const bf16x8* dp = stage + dslot * NK * 64 + lane;
+  const bf16x8* xp = stage + xslot * NK * 64 + lane;
   f32x16 acc = zero16();
+  bf16x8 da = dp[0], xa = xp[0];
 #pragma unroll
-  for (int w = 0; w < PW_NW; ++w)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      acc = Tr<bf16_t>::mma(stage[((dslot * PW_NW + w) * 2 + s) * 64 + lane],
-                            stage[((xslot * PW_NW + w) * 2 + s) * 64 + lane], acc);
-  const int ci = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int o = g * 1024 + cl_x(r, h) * 32 + ci;
-    slab_p[o] = slabl[o] + acc[r];
+  for (int k = 0; k < NK; ++k) {
+    bf16x8 dn = da, xn = xa;
+    if (k + 1 < NK) { dn = dp[(k + 1) * 64]; xn = xp[(k + 1) * 64]; }
+    acc = Tr<bf16_t>::mma(da, xa, acc);
+    da = dn; xa = xn;
   }
+  // one base per lane + compile-time offsets (cl_x(r, h) = cl_x(r, 0) + 4 h)
+  const int ci = lane & 31, h = lane >> 5;
+  const int o = g * 1024 + 4 * h * 32 + ci;
+  float* sp = slab_p + o;
+  const float* sl = slabl + o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sp[cl_x(r, 0) * 32] = sl[cl_x(r, 0) * 32] + acc[r];
 }
 
 // Add one row's 1x1 weight-gradient tile (dW[n][ci] = sum_p D[p][n] X[p][ci],
@@ -719,7 +737,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float kap = a.kappa[c], gam = a.gamma[c], bw1 = a.bnw1[c], bb1 = a.bnb1[c];
   const float m1 = stat[64 + c], rs1 = stat[96 + c];
-  const float ba = a.gb[0][c] + a.gb[1][c], be = a.gb[4][c] + a.gb[5][c];
+  const float nba = sig_nb(a.gb[0][c] + a.gb[1][c]), nbe = sig_nb(a.gb[4][c] + a.gb[5][c]);
 
   // close frame t-1 (:172-175)
   f32x16 Ep = zero16();
@@ -748,7 +766,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
   acc = gemm_pa<S>(pae, a.gf[1], acc, lane);
   f32x16 att, gEv;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { att[r] = sigm(acc[r] + ba); gEv[r] = att[r] * Ep[r]; }
+  for (int r = 0; r < 16; ++r) { att[r] = sigm_b(acc[r], nba); gEv[r] = att[r] * Ep[r]; }
   if (sizeof(S) == 4 && (a.ablate & 8192))
 #pragma unroll
     for (int r = 0; r < 16; ++r) gEv[r] = (float)(bf16_t)gEv[r];
@@ -776,7 +794,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
   acc = gemm_pa<S>(pag, a.gf[5], acc, lane);
   f32x16 egn;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) egn[r] = sigm(acc[r] + be);
+  for (int r = 0; r < 16; ++r) egn[r] = sigm_b(acc[r], nbe);
   if (sizeof(S) == 4 && (a.ablate & 8192))
 #pragma unroll
     for (int r = 0; r < 16; ++r) egn[r] = (float)(bf16_t)egn[r];
@@ -840,7 +858,7 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, 
   const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
   const float m0 = stat[c], rs0 = stat[32 + c];
   const float A0 = bw0 * rs0, B0 = bb0 - bw0 * rs0 * m0;     // BN0 affine folded
-  const float bi = a.gb[2][c] + a.gb[3][c];
+  const float nbi = sig_nb(a.gb[2][c] + a.gb[3][c]);
 
   f32x16 z, xv, ih;
   stem_cl<ACT>(xs, yl, h, st, z, xv);
@@ -858,7 +876,7 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, 
   f32x16 In;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const float ig = sigm(acc[r] + bi);
+    const float ig = sigm_b(acc[r], nbi);
     In[r] = (1.f - ig) * (float)in.Iv[r] + ig * ih[r];
   }
   if (sizeof(S) == 4 && (a.ablate & 4096))
@@ -935,7 +953,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   const int slots[9] = {SM_GBA, SM_KAPPA, SM_GAMMA, SM_BN1W, SM_BN1B, SM_PW0, SM_PW1, SM_PW2, SM_PB};
   float bs0 = 0.f, bs1 = 0.f;   // BN1 bwd partial sums
 
-  const float ba = a.gb[0][c] + a.gb[1][c];
+  const float nba = sig_nb(a.gb[0][c] + a.gb[1][c]);
   const float kap = a.kappa[c], gam = a.gamma[c], bw1 = a.bnw1[c], bb1 = a.bnb1[c];
   float m1 = 0.f, rs1 = 0.f;
   if (head) { m1 = a.bnstat[(size_t)t * 128 + 64 + c]; rs1 = a.bnstat[(size_t)t * 128 + 96 + c]; }
@@ -947,8 +965,8 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 GE;
     if (tail) {
-      f32x16 z, xv;
-      stem_cl<ACT>(L.xs, yl, h, st, z, xv);
+      f32x16 z, xv;                          // z: nl'(stem pre-activation)
+      stem_cl<ACT, true>(L.xs, yl, h, st, z, xv);
       // this kernel's share of d xbn_tt (a_w^T d_att_pre); k_pw_bb adds the
       // inhibition path's share to the same stem-gradient sums itself (the
       // stem gradient is linear in d xbn), so no d xbn tile crosses HBM
@@ -968,7 +986,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
         f32x16 att, dap;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          att[r] = sigm(g[r] + ba);
+          att[r] = sigm_b(g[r], nba);
           const float datt = HG ? dgE[r] * Et[r] + (float)dAt[r] : dgE[r] * Et[r];
           dap[r] = datt * att[r] * (1.f - att[r]);
           sm[0] += dap[r];
@@ -988,7 +1006,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const f32x4 xin = L.xs[yl * IMG + cl_x(r, h)];
-        const float dz = dx[r] * Act<ACT>::d(z[r]);
+        const float dz = dx[r] * z[r];
         sm[5] += dz * xin[0]; sm[6] += dz * xin[1]; sm[7] += dz * xin[2]; sm[8] += dz;
       }
     } else {
@@ -1102,7 +1120,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
   const float m0 = bs[c], rs0 = bs[32 + c];
-  const float bi = a.gb[2][c] + a.gb[3][c];
+  const float nbi = sig_nb(a.gb[2][c] + a.gb[3][c]);
   float sm[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int slots[10] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B,
                          SM_PW0, SM_PW1, SM_PW2, SM_PB};
@@ -1146,8 +1164,8 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
       const f32x16 dEn = gemm_pa<S>(pe, a.gt[4], load_cl(a.dEn + ro, c, h), lane);
       store_cl(a.dEn + ro, c, h, dEn);
     } else {
-      f32x16 z, xv;
-      stem_cl<ACT>(L.xs, yl, h, st, z, xv);
+      f32x16 z, xv;                          // z: nl'(stem pre-activation)
+      stem_cl<ACT, true>(L.xs, yl, h, st, z, xv);
       f32x16 g = zero16();
       {
         F pax[Tr<S>::KS], pai[Tr<S>::KS];
@@ -1170,7 +1188,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         Act<ACT>::fd(p, fp, dfp);
         const float q = xv[r] - fp;
         Act<ACT>::fd(q, ih, dfq);
-        const float ig = sigm(g[r] + bi);
+        const float ig = sigm_b(g[r], nbi);
         const float dih = dIr * ig;
         dip[r] = dIr * (ih - Ip) * ig * (1.f - ig);
         const float dq = dih * dfq;
@@ -1209,7 +1227,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const f32x4 xin = L.xs[yl * IMG + cl_x(r, h)];
-        const float dz = dx[r] * Act<ACT>::d(z[r]);
+        const float dz = dx[r] * z[r];
         sm[6] += dz * xin[0]; sm[7] += dz * xin[1]; sm[8] += dz * xin[2]; sm[9] += dz;
       }
       dIp = gemm_pa<S>(pd, a.gt[3], dIp, lane);

@@ -230,6 +230,13 @@ __device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x
 __device__ __forceinline__ float flog(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float sigm(float x) { return frcp(1.f + fexp(-x)); }
+// sigmoid(x + b) with nb = sig_nb(b) precomputed: the bias add and the 2^x
+// scaling fold into one FMA
+constexpr float L2E = 1.4426950408889634f;
+__device__ __forceinline__ float sig_nb(float b) { return -b * L2E; }
+__device__ __forceinline__ float sigm_b(float x, float nb) {
+  return frcp(1.f + __builtin_amdgcn_exp2f(fmaf(x, -L2E, nb)));
+}
 __device__ __forceinline__ float ftanh(float x) {
   const float t = 1.f - 2.f * frcp(fexp(2.f * fabsf(x)) + 1.f);
   return copysignf(t, x);
