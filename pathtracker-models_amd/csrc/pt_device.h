@@ -415,9 +415,6 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
 // column kw+1 is fetched from L2 into registers at the top of column kw and
 // written to LDS after its MFMAs, so no MFMA ever waits on an L2 round trip
 // and each workgroup reads the weights once instead of once per wave.
-#ifndef PT_CONV_PRIO
-#define PT_CONV_PRIO 0               // experiments: 1 static s_setprio for the younger half, 2 per MFMA cluster
-#endif
 constexpr int CONV_PF = 3;          // A-fragment prefetch depth (tile rows)
 constexpr int WSLICE_CHUNKS = 896;   // 16-B chunks per slice: 7 taps x 2 x 64 x 16 B (bf16)
                                      //                       = 7 taps x 8 x 64 x 4 B (f32, per pass)
@@ -490,9 +487,6 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
   constexpr int off = PAD - K / 2;
   constexpr int NTR = RW + K - 1;           // tile rows touched by this wave
   const int h = lane >> 5, px = lane & 31;
-#if PT_CONV_PRIO == 1
-  if (__builtin_amdgcn_readfirstlane(tid) >= NTH / 2) __builtin_amdgcn_s_setprio(1);
-#endif
   for (int pass = 0; pass < TT::NPASS; ++pass) {
     WSlice pre;
     if constexpr (LDSW) wslice_load<S, K, NTH>(pre, wf, pass, 0, tid);
@@ -539,9 +533,6 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
       for (int tr = 0; tr < NTR; ++tr) {
         if (tr + PF < NTR) load_a(tr + PF);
         __builtin_amdgcn_sched_barrier(0);
-#if PT_CONV_PRIO == 2
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int s = 0; s < KSP; ++s) {
           // D^T[n][p] += W[n][k] X^T[k][p]: weights on A, pixels on B -> PL output
@@ -551,9 +542,6 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
             if (i >= 0 && i < RW) acc[i] = TT::mma(bc[kh][s], av[tr][s], acc[i]);
           }
         }
-#if PT_CONV_PRIO == 2
-        __builtin_amdgcn_s_setprio(0);
-#endif
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (Done::active) {
           const int i = tr - (K - 1);
