@@ -240,8 +240,11 @@ __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps
   }
 }
 
-// Per-clip (mean, M2) of the conv outputs held in acc (PL layout, two-pass,
-// robust), accumulated into the fp64 batch sums.  red: 256 floats.
+// Per-clip (mean, M2) of the conv outputs held in acc (PL layout), accumulated
+// into the fp64 batch sums.  Each wave runs a two-pass (mean, M2) over its own
+// RW rows (its per-channel means go through its own LDS slot, no workgroup
+// barrier); one barrier, then Chan's combination over the NW equal-sized wave
+// blocks: M2 = sum M2_w + n_w sum (mean_w - mean)^2.  red: 2 * NW * 32 floats.
 template <int RW, int NW>
 __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out, int lane,
                                int wave, int tid, int ablate) {
@@ -251,16 +254,15 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out,
 #pragma unroll
   for (int i = 1; i < RW; ++i) s += acc[i];
   const float ts = pl_lane_sum(s, lane);
-  if (!(lane & 16)) red[wave * 32 + ch] = ts;
-  __syncthreads();
+  float* rw = red + wave * 32;                       // this wave's block means
+  if (!(lane & 16)) rw[ch] = ts * (1.f / (RW * IMG));
+  wave_sync();
   f32x16 mean;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    f32x4 m = *(const f32x4*)(red + 8 * g + 4 * h);
+    const f32x4 m = *(const f32x4*)(rw + 8 * g + 4 * h);
 #pragma unroll
-    for (int w = 1; w < NW; ++w) m += *(const f32x4*)(red + w * 32 + 8 * g + 4 * h);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) mean[4 * g + j] = m[j] * (1.f / NPIX);
+    for (int j = 0; j < 4; ++j) mean[4 * g + j] = m[j];
   }
   f32x16 q = zero16();
 #pragma unroll
@@ -272,13 +274,22 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out,
   if (!(lane & 16)) red[NW * 32 + wave * 32 + ch] = tq;
   __syncthreads();
   if (tid < 32 && !(ablate & 32768)) {
-    float sm = 0.f, v = 0.f;
+    float mn = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) { sm += red[w * 32 + tid]; v += red[NW * 32 + w * 32 + tid]; }
-    const double mn = (double)(sm * (1.f / NPIX));
+    for (int w = 0; w < NW; ++w) mn += red[w * 32 + tid];
+    mn *= 1.f / NW;
+    float v = 0.f, dv = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float d = red[w * 32 + tid] - mn;
+      v += red[NW * 32 + w * 32 + tid];
+      dv += d * d;
+    }
+    v += dv * (float)(RW * IMG);
+    const double md = (double)mn;
     out += (blockIdx.x % NBNC) * 96;
-    unsafeAtomicAdd(out + tid, mn);
-    unsafeAtomicAdd(out + 32 + tid, mn * mn);
+    unsafeAtomicAdd(out + tid, md);
+    unsafeAtomicAdd(out + 32 + tid, md * md);
     unsafeAtomicAdd(out + 64 + tid, (double)v);
   }
 }

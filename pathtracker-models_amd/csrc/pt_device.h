@@ -182,17 +182,35 @@ __device__ __forceinline__ int pl_sum_reg(int lane) {
   const int q = lane & 15;
   return 8 * (q & 1) + 4 * ((q >> 1) & 1) + 2 * ((q >> 2) & 1) + ((q >> 3) & 1);
 }
+// Each halving step selects between two NAMED values: written as
+// (b ? v[j + 8] : v[j]) LLVM folds the pair into one dynamic element index and
+// lowers it as a 16-way compare/select chain (~1200 VALU per wave in the conv
+// epilogue, ~4.6 us per launch); pin() keeps both extracts static.
+__device__ __forceinline__ void pin(float& x, float& y) { asm volatile("" : "+v"(x), "+v"(y)); }
 __device__ __forceinline__ float pl_lane_sum(const f32x16& v, int lane) {
   float a[8], b[4], c[2];
   const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    a[j] = (b0 ? v[j + 8] : v[j]) + __shfl_xor(b0 ? v[j] : v[j + 8], 1);
+  for (int j = 0; j < 8; ++j) {
+    float lo = v[j], hi = v[j + 8];
+    pin(lo, hi);
+    a[j] = (b0 ? hi : lo) + __shfl_xor(b0 ? lo : hi, 1);
+  }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) b[j] = (b1 ? a[j + 4] : a[j]) + __shfl_xor(b1 ? a[j] : a[j + 4], 2);
+  for (int j = 0; j < 4; ++j) {
+    float lo = a[j], hi = a[j + 4];
+    pin(lo, hi);
+    b[j] = (b1 ? hi : lo) + __shfl_xor(b1 ? lo : hi, 2);
+  }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) c[j] = (b2 ? b[j + 2] : b[j]) + __shfl_xor(b2 ? b[j] : b[j + 2], 4);
-  float d = (b3 ? c[1] : c[0]) + __shfl_xor(b3 ? c[0] : c[1], 8);
+  for (int j = 0; j < 2; ++j) {
+    float lo = b[j], hi = b[j + 2];
+    pin(lo, hi);
+    c[j] = (b2 ? hi : lo) + __shfl_xor(b2 ? lo : hi, 4);
+  }
+  float lo = c[0], hi = c[1];
+  pin(lo, hi);
+  const float d = (b3 ? hi : lo) + __shfl_xor(b3 ? lo : hi, 8);
   return d + __shfl_xor(d, 16);
 }
 
