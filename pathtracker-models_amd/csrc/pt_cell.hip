@@ -341,8 +341,51 @@ struct StoreRow {
   S* base;
   int h;
   static constexpr bool active = true;
+  static constexpr bool prefetch_active = false;
+  __device__ __forceinline__ void prefetch() const {}
   __device__ __forceinline__ void operator()(int i, const f32x16& v) const {
     store_pl(base + (size_t)i * IMG * C, h, v);
+  }
+};
+
+// conv_run row hook of EPI_ADD (bf16): the add0 / add1 rows of this wave are
+// prefetched into registers under the MFMA loop (issued at the first column);
+// each output row is summed and stored as soon as its last MFMA retires.
+// (Loaded after the loop, the 256 workgroups' add/store burst cost conv_bb
+// 11 us and conv_ba 7 us per launch.)
+template <int RW>
+struct AddRowBf16 {
+  bf16_t* out;
+  const bf16_t *add0, *add1;      // add1 may be null
+  size_t po;                      // element offset of row 0 of this lane's pixel
+  int h;
+  bf16x4 (&p0)[RW][4];
+  bf16x4 (&p1)[RW][4];
+  static constexpr bool active = true;
+  static constexpr bool prefetch_active = true;
+  __device__ __forceinline__ void prefetch() const {
+#pragma unroll
+    for (int i = 0; i < RW; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) p0[i][g] = *(const bf16x4*)(add0 + po + (size_t)i * IMG * C + 8 * g + 4 * h);
+    if (add1)
+#pragma unroll
+      for (int i = 0; i < RW; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) p1[i][g] = *(const bf16x4*)(add1 + po + (size_t)i * IMG * C + 8 * g + 4 * h);
+  }
+  __device__ __forceinline__ void operator()(int i, const f32x16& acc) const {
+    f32x16 v = acc;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * g + j] += (float)p0[i][g][j];
+    if (add1)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * g + j] += (float)p1[i][g][j];
+    store_pl(out + po + (size_t)i * IMG * C, h, v);
   }
 };
 
@@ -458,6 +501,11 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate, sr);
       if (a.ablate & 256) return;
       if (!(a.ablate & 8)) bn_fwd_partial<RW, NW>(acc, red, a.bnacc, lane, wave, tid, a.ablate);
+    } else if constexpr (sizeof(S) == 2) {
+      bf16x4 p0[RW][4], p1[RW][4];
+      const AddRowBf16<RW> ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
+                              cb + ((size_t)(wave * RW) * IMG + px) * C, h, p0, p1};
+      conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate, ar);
     } else {
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate);
       if (a.ablate & 256) return;

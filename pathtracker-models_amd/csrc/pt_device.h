@@ -485,9 +485,14 @@ __device__ __forceinline__ void wslice_store(WSlice& r, char* buf, int tid) {
 // Row-final hook: called as done(i, acc[i]) the moment output row i has
 // received its last MFMA (last pass, last kernel column, tile row i + K - 1),
 // so an epilogue can store row i while the later rows' MFMAs still run.
+// A hook may also prefetch (prefetch_active): called once, at the first kernel
+// column right after the next weight slice's loads are issued, so the loads
+// it issues overlap the MFMA loop and never delay the fill or the slices.
 struct NoRowHook {
   __device__ __forceinline__ void operator()(int, const f32x16&) const {}
+  __device__ __forceinline__ void prefetch() const {}
   static constexpr bool active = false;
+  static constexpr bool prefetch_active = false;
 };
 
 // k > 7 (PAD = PADBIG): the 46 x 46 tile leaves no LDS for weight slices;
@@ -518,6 +523,8 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
       if constexpr (LDSW) {
         const F* wl = (const F*)(wbuf + (kw & 1) * WSLICE_BYTES) + lane;
         if (kw + 1 < K && !(ablate & 16384)) wslice_load<S, K, NTH>(pre, wf, pass, kw + 1, tid);
+        if constexpr (Done::prefetch_active)
+          if (kw == 0 && pass == TT::NPASS - 1) done.prefetch();
 #pragma unroll
         for (int kh = 0; kh < K; ++kh)
 #pragma unroll
@@ -528,6 +535,8 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
 #pragma unroll
           for (int s = 0; s < KSP; ++s)
             bc[kh][s] = wf[((kh * K + kw) * TT::KS + pass * KSP + s) * 64 + lane];
+        if constexpr (Done::prefetch_active)
+          if (kw == 0 && pass == TT::NPASS - 1) done.prefetch();
       }
       const int tcol = px + kw + off;
       // A fragments of tile row tr, software-pipelined CONV_PF rows ahead of
