@@ -493,6 +493,7 @@ struct NoRowHook {
   __device__ __forceinline__ void prefetch() const {}
   static constexpr bool active = false;
   static constexpr bool prefetch_active = false;
+  static constexpr bool wreg = false;
 };
 
 // k > 7 (PAD = PADBIG): the 46 x 46 tile leaves no LDS for weight slices;
@@ -505,11 +506,23 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
                                            const Done& done = Done()) {
   using TT = Tr<S>;
   using F = typename TT::frag;
-  constexpr bool LDSW = K <= 2 * PADMAX + 1;  // weight slices staged in LDS
+  // Done::wreg (k <= 7): each wave reads its B fragments from L2 into
+  // registers one column ahead instead of the LDS slice ring -- no
+  // workgroup barrier per column
+  constexpr bool WREG = Done::wreg && K <= 2 * PADMAX + 1;
+  constexpr bool LDSW = K <= 2 * PADMAX + 1 && !WREG;  // weight slices staged in LDS
   constexpr int KSP = TT::KS / TT::NPASS;   // k-steps per pass per tap
   constexpr int off = PAD - K / 2;
   constexpr int NTR = RW + K - 1;           // tile rows touched by this wave
   const int h = lane >> 5, px = lane & 31;
+  F bn[K][KSP];                             // WREG: the next column's fragments
+  auto load_col = [&](int pass, int kw) {
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+      for (int s = 0; s < KSP; ++s) bn[kh][s] = wf[((kh * K + kw) * TT::KS + pass * KSP + s) * 64 + lane];
+  };
+  if constexpr (WREG) load_col(0, 0);
   for (int pass = 0; pass < TT::NPASS; ++pass) {
     WSlice pre;
     if constexpr (LDSW) wslice_load<S, K, NTH>(pre, wf, pass, 0, tid);
@@ -529,6 +542,15 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
         for (int kh = 0; kh < K; ++kh)
 #pragma unroll
           for (int s = 0; s < KSP; ++s) bc[kh][s] = wl[(kh * KSP + s) * 64];
+      } else if constexpr (WREG) {
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+          for (int s = 0; s < KSP; ++s) bc[kh][s] = bn[kh][s];
+        if (kw + 1 < K) load_col(pass, kw + 1);
+        else if (pass + 1 < TT::NPASS) load_col(pass + 1, 0);
+        if constexpr (Done::prefetch_active)
+          if (kw == 0 && pass == TT::NPASS - 1) done.prefetch();
       } else {
 #pragma unroll
         for (int kh = 0; kh < K; ++kh)
