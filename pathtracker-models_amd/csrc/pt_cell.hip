@@ -1371,18 +1371,19 @@ __device__ __forceinline__ bf16x8 tr_read8(const bf16_t* p) {
 // One band = (frame, clip, RB D rows): the X rows y0-PAD .. y0+RB-1+PAD
 // (interior columns; the PAD halo columns each side stay zero from the
 // initial clear, rows outside the image are written as zeros) and the D rows.
-template <class S, int PAD>
+template <class S, int PAD, int NTH = NT>
 struct WBand {
   static constexpr int CPB = 16 / (int)sizeof(S);
   static constexpr int NCH = C / CPB;
   static constexpr int RB = wg_rb<S, PAD>(), XR = wg_xr<S, PAD>();
-  static constexpr int XPER = XR * IMG * NCH / NT;     // 7 / 10 (PAD 3), 9 / 16 (PAD 7)
-  static constexpr int DPER = RB * IMG * NCH / NT;     // 4 / 4, 2 / 2
-  static_assert(XR * IMG * NCH % NT == 0 && RB * IMG * NCH % NT == 0, "band split");
+  static constexpr int XN = XR * IMG * NCH;            // X chunks (the last pass may be partial)
+  static constexpr int XPER = (XN + NTH - 1) / NTH;    // 7 / 10 (PAD 3), 9 / 16 (PAD 7) at NT
+  static constexpr int DPER = RB * IMG * NCH / NTH;    // 4 / 4, 2 / 2
+  static_assert(RB * IMG * NCH % NTH == 0, "band split");
   // tiled frames only: the 2 PAD halo columns of the X rows come from the left /
   // right neighbour tiles (at 32x32 they stay zero from the initial clear)
   static constexpr int HN = XR * 2 * PAD * NCH;
-  static constexpr int HPER = (HN + NT - 1) / NT;
+  static constexpr int HPER = (HN + NTH - 1) / NTH;
   u32x4 x[XPER], d[DPER], hx[HPER];
   int xvalid;                                              // bit j: X chunk j inside the frame
   int hvalid;                                              // bit j: halo chunk j inside the frame
@@ -1396,12 +1397,13 @@ struct WBand {
     xvalid = 0;
 #pragma unroll
     for (int j = 0; j < XPER; ++j) {
-      const int idx = tid + j * NT;
+      const bool in = XN % NTH == 0 || tid + j * NTH < XN;
+      const int idx = in ? tid + j * NTH : 0;
       const int q = idx % NCH, pc = idx / NCH;
       const int col = pc % IMG, row = pc / IMG;
       const int iy = y0 + row - PAD;
       const int dy = iy < 0 ? -1 : (iy >= IMG ? 1 : 0);
-      const bool ok = L.ty + dy >= 0 && L.ty + dy < nty;
+      const bool ok = in && L.ty + dy >= 0 && L.ty + dy < nty;
       const int cy = ok ? iy - dy * IMG : 0;
       x[j] = *(const u32x4*)(xfr + clip_off(ok ? b + dy * ntx : b) + (cy * IMG + col) * C + q * CPB);
       xvalid |= ok << j;
@@ -1410,7 +1412,7 @@ struct WBand {
     if (ntx * nty > 1) {
 #pragma unroll
       for (int j = 0; j < HPER; ++j) {
-        const int idx = tid + j * NT;
+        const int idx = tid + j * NTH;
         const int q = idx % NCH, pc = idx / NCH;
         const int k = pc % (2 * PAD), row = pc / (2 * PAD);
         const int ix = k < PAD ? k - PAD : IMG + k - PAD;
@@ -1426,7 +1428,7 @@ struct WBand {
     }
 #pragma unroll
     for (int j = 0; j < DPER; ++j) {
-      const int idx = tid + j * NT;
+      const int idx = tid + j * NTH;
       const int q = idx % NCH, pc = idx / NCH;
       d[j] = *(const u32x4*)(dsrc + (y0 * IMG + pc) * C + q * CPB);
     }
@@ -1434,7 +1436,8 @@ struct WBand {
   __device__ __forceinline__ void store(S* xt, S* dt, int tid, bool tiled) const {
 #pragma unroll
     for (int j = 0; j < XPER; ++j) {
-      const int idx = tid + j * NT;
+      const int idx = tid + j * NTH;
+      if (XN % NTH != 0 && idx >= XN) break;
       const int q = idx % NCH, pc = idx / NCH;
       const int col = pc % IMG, row = pc / IMG;
       const u32x4 z = {0u, 0u, 0u, 0u};
@@ -1443,7 +1446,7 @@ struct WBand {
     if (tiled) {
 #pragma unroll
       for (int j = 0; j < HPER; ++j) {
-        const int idx = tid + j * NT;
+        const int idx = tid + j * NTH;
         const int q = idx % NCH, pc = idx / NCH;
         const int k = pc % (2 * PAD), row = pc / (2 * PAD);
         const int col = k < PAD ? k : IMG + k;
@@ -1453,7 +1456,7 @@ struct WBand {
     }
 #pragma unroll
     for (int j = 0; j < DPER; ++j) {
-      const int idx = tid + j * NT;
+      const int idx = tid + j * NTH;
       const int q = idx % NCH, pc = idx / NCH;
       *(u32x4*)(dt + pc * C + q * CPB) = d[j];
     }
@@ -1533,10 +1536,12 @@ __device__ __forceinline__ void wgrad_band2(f32x16 (&acc)[WG2_NACC], const bf16_
   }
 }
 
-template <class S, int PAD, class Body>
+// NTH threads per workgroup, all of them staging the bands.
+template <class S, int PAD, int NTH = NT, class Body>
 __device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
                                           const S* __restrict__ Ds, int B, int T, int g, int nwg,
                                           S* buf, int tid, int ablate, int ntx, int nty) {
+  constexpr bool stager = true;                  // every thread stages its share
   const bool tiled = ntx * nty > 1;
   constexpr int BE = wgrad_band_elems<S, PAD>();
   constexpr int NBUF = wg_nbuf<S, PAD>();
@@ -1546,11 +1551,11 @@ __device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
   const int npairs = (B * T - g + nwg - 1) / nwg;
   const int nunits = npairs * NB;
   // clear the buffers once (the X halo columns stay zero)
-  for (int i = tid; i < NBUF * BE * (int)sizeof(S) / 16; i += NT)
+  for (int i = tid; i < NBUF * BE * (int)sizeof(S) / 16; i += NTH)
     ((u32x4*)buf)[i] = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
-  WBand<S, PAD> band;
-  if (nunits > 0) {
+  WBand<S, PAD, NTH> band;
+  if (nunits > 0 && stager) {
     band.load(Xs, Ds, B, g, 0, tid, ntx, nty);
     band.store(buf, buf + XE, tid, tiled);
   }
@@ -1563,17 +1568,17 @@ __device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
     // one buffer (f32, PAD 7): load it after (the staged band would not fit
     // in registers beside the accumulators)
     if constexpr (NBUF == 2)
-      if (more && !(ablate & 128))
+      if (more && stager && !(ablate & 128))
         band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * RB, tid, ntx, nty);
     if (!(ablate & 64)) body(xt, dt);
     if (more) {
       S* xn = buf + (NBUF == 2 ? ((u + 1) & 1) * BE : 0);
       if constexpr (NBUF == 1) {
         __syncthreads();                              // every wave is done reading the buffer
-        if (!(ablate & 128))
+        if (stager && !(ablate & 128))
           band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * RB, tid, ntx, nty);
       }
-      if (!(ablate & 128)) band.store(xn, xn + XE, tid, tiled);
+      if (stager && !(ablate & 128)) band.store(xn, xn + XE, tid, tiled);
       __syncthreads();
     }
   }
@@ -1586,8 +1591,15 @@ __device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
 // The D / X row bands are staged in LDS; per-workgroup partials go to wslab
 // [2][nwg][K*K][1024].  grid = (nwg, convs, tap groups).
 // =========================================================================
+// bf16, k <= 7: 8 waves (WG8_NT threads), wave w owns kernel column w (7
+// accumulator tiles), two waves per SIMD hide each other's LDS waits; the
+// 4-wave form (two columns per wave, one wave per SIMD) serves k > 7 and f32.
+constexpr int WG8_NT = 512;
+template <class S, int PAD> constexpr int wgrad_nt() { return sizeof(S) == 2 && PAD == PADMAX ? WG8_NT : NT; }
 template <class S, int PAD>
-__global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, int nwg, int conv0) {
+__global__ __launch_bounds__((wgrad_nt<S, PAD>()), 1) void k_wgrad(CellArgs<S> a, float* wslab, int nwg, int conv0) {
+  constexpr int NTH = wgrad_nt<S, PAD>();
+  constexpr int NKW = NTH == WG8_NT ? 1 : 2;        // kernel columns per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   S* buf = (S*)smem;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
@@ -1605,14 +1617,17 @@ __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, in
     for (int m = 0; m < WG2_NACC; ++m) acc[m] = zero16();
     const int nkwg = (a.K + 7) / 8;                  // column groups (1 for k <= 7)
     const int kh0 = PAD == PADMAX ? 0 : (grp / nkwg) * 7;
-    const int kw0 = (PAD == PADMAX ? 0 : (grp % nkwg) * 8) + 2 * wave;
+    const int kw0 = (PAD == PADMAX ? 0 : (grp % nkwg) * 8) + NKW * wave;
     auto run = [&](auto kc) {
       constexpr int K = decltype(kc)::value;
-      // every wave runs two columns; a column kw >= K (wave 3's second at
-      // K = 7) reads in-bounds LDS and its tiles are never stored: uniform
-      // code, and that wave is otherwise idle while the others finish
-      wgrad_run<S, PAD>(
-          [&](const S* xt, const S* dt) { wgrad_band2<K, 2, PAD>(acc, xt, dt, kw0, kh0, lane); },
+      // 4 waves: every wave runs two columns; a column kw >= K (wave 3's
+      // second at K = 7) reads in-bounds LDS and its tiles are never stored.
+      // 8 waves: a wave whose column is >= K only stages and syncs.
+      wgrad_run<S, PAD, NTH>(
+          [&](const S* xt, const S* dt) {
+            if (NKW == 1 && kw0 >= K) return;
+            wgrad_band2<K, NKW, PAD>(acc, xt, dt, kw0, kh0, lane);
+          },
           Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
     };
     if constexpr (PAD == PADMAX) {
@@ -1632,7 +1647,7 @@ __global__ __launch_bounds__(NT, 1) void k_wgrad(CellArgs<S> a, float* wslab, in
     }
     // acc[j * 7 + kh - kh0]: rows ci = cl_x(r,h), cols n = lane&31
 #pragma unroll
-    for (int m = 0; m < WG2_NACC; ++m) {
+    for (int m = 0; m < 7 * NKW; ++m) {
       const int kh = kh0 + m % 7, kw = kw0 + m / 7;
       if (kh < a.K && kw < a.K) {
 #pragma unroll
@@ -2281,7 +2296,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   timed(PT_K_WGRAD, st, [&] {
     const dim3 grid(p.nwg, 2 - conv0, wgrad_groups(p.K, sizeof(S) == 2));
     if (p.K <= 2 * PADMAX + 1)
-      hipLaunchKernelGGL((k_wgrad<S, PADMAX>), grid, dim3(NT), (wgrad_lds_bytes<S, PADMAX>()), st, a,
+      hipLaunchKernelGGL((k_wgrad<S, PADMAX>), grid, dim3(wgrad_nt<S, PADMAX>()), (wgrad_lds_bytes<S, PADMAX>()), st, a,
                          wslab, p.nwg, conv0);
     else
       hipLaunchKernelGGL((k_wgrad<S, PADBIG>), grid, dim3(NT), (wgrad_lds_bytes<S, PADBIG>()), st, a,
