@@ -41,11 +41,15 @@ constexpr int HC = 32;             // padded hidden / input channels
 constexpr int NG = 4;              // gates i, f, c, o
 constexpr int GC = NG * HC;        // 128
 constexpr int KMAX = 15;
-// output rows per conv workgroup: 8 for the 4-gate forward (one gate tile per
-// wave, 8 rows each), the whole image for the 4-gates-in transposed conv (one
-// output tile: each wave takes 8 rows, so both variants reuse every LDS
-// fragment across up to 8 output rows)
-template <int NO> constexpr int conv_rb() { return NO == 4 ? 8 : IMG; }
+// output rows per conv workgroup: 4 for the 4-gate forward (one gate tile per
+// wave, 4 rows each: 132 VGPRs, two workgroups per CU hide each other's
+// column-start waits; 8 rows at one wave per SIMD ran 120 us per launch), the
+// whole image for the 4-gates-in transposed conv (one output tile: each wave
+// takes 8 rows, reusing every LDS fragment across 8 output rows)
+template <int NO> constexpr int conv_rb() { return NO == 4 ? 4 : IMG; }
+// workgroups per CU the register budget allows (NO = 4: 4 rows per wave, two
+// waves per SIMD; NO = 1: 8 rows per wave over 4 input groups, one)
+template <int NO> constexpr int conv_occ() { return NO == 4 ? 2 : 1; }
 
 // ------------------------------------------------------------------ conv tile
 template <class S, int K, int RB> struct LTile {
@@ -82,7 +86,7 @@ struct LConvArgs {
 // kw, k-step) is read from LDS once and feeds the K MFMAs of the output rows
 // it contributes to.  Wave w: output tile o = w % NO, rows (w / NO) * RW ...
 template <class S, int K, int NI, int NO>
-__global__ __launch_bounds__(NT, 1) void k_lconv(LConvArgs a) {
+__global__ __launch_bounds__(NT, conv_occ<NO>()) void k_lconv(LConvArgs a) {
   using TT = Tr<S>;
   using F = typename TT::frag;
   constexpr int RB = conv_rb<NO>(), NBAND = IMG / RB;
