@@ -119,6 +119,41 @@ int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params*
                      const void* saved, void* workspace, const float* d_e_last,
                      const pt_cell_grads* g, pt_stream_t stream);
 
+/* Cross-replica hooks (one process per GPU).  Pass NULL for
+ * the reference's DataParallel semantics (per-replica BatchNorm statistics,
+ * mainclean.py:132-134) and a single-stream backward.
+ *
+ *  bn_world > 1: SyncBN.  After each BatchNorm reduction (2 per frame forward,
+ *    2 per frame backward) the library writes the replica's batch totals to
+ *    bn_buf[offset, offset + count) (device, caller-owned, at least
+ *    pt_cell_bn_sync_doubles() doubles) and calls allreduce(user, offset,
+ *    count), which must enqueue, on the call's stream, a SUM of those doubles
+ *    over the bn_world replicas and return 0; the statistics then cover all
+ *    replicas' clips (count B * bn_world), so the replicas together compute
+ *    exactly the single-process batch's forward and gradients (each on its
+ *    own clips).  The call is made from the thread that called the entry
+ *    point, between kernel launches; hipGraph replay is off in this mode.
+ *  grads_early_event (hipEvent_t or NULL): recorded on the stream by the
+ *    backward once every gradient except w_exc / w_inh is written, before the
+ *    k x k weight-gradient kernel: the caller can all-reduce those gradients
+ *    on another stream while that kernel runs (pt_cell_backward_dist). */
+typedef int (*pt_bn_allreduce_fn)(void* user, int64_t offset, int64_t count);
+typedef struct pt_cell_dist {
+    int32_t bn_world;
+    double* bn_buf;
+    pt_bn_allreduce_fn allreduce;
+    void* user;
+    void* grads_early_event;
+} pt_cell_dist;
+
+size_t pt_cell_bn_sync_doubles(const pt_cell_desc* d);
+int pt_cell_forward_dist(const pt_cell_desc* d, const void* x, const pt_cell_params* p,
+                         void* saved, void* workspace, float* e_last, float* gates,
+                         const pt_cell_dist* dist, pt_stream_t stream);
+int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_params* p,
+                          const void* saved, void* workspace, const float* d_e_last,
+                          const pt_cell_grads* g, const pt_cell_dist* dist, pt_stream_t stream);
+
 /* Optional kernel timing for benchmarks (process-wide, off by default; the
  * only mutable library state, guarded by a mutex).  When enabled for a kernel
  * kind, every launch of that kind is bracketed by two hipEvents on its launch

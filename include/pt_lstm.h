@@ -94,6 +94,12 @@ int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace,
 int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace, float mu,
                        float* jv, pt_lstm_stream_t stream);
 
+/* Per-step hidden states h_t, t = 0..T-1, of the forward that filled `saved`,
+ * as fp32 [B,ch,T,H,W] (testmode outputs of the clip ConvLSTM: the reference
+ * ConvLSTM's testmode collects the per-step h, models/convlstm.py:127-135). */
+int pt_lstm_export_h(const pt_lstm_desc* d, const void* saved, float* h_seq,
+                     pt_lstm_stream_t stream);
+
 /* Frame stem of the clip ConvLSTM (the stem of InT.py:192,212-213
  * applied per frame): y = softplus(W x + b), a 1x1x1 channel mix over the n
  * voxels of the clip batch into y [B,cout,n] (n = T*H*W, a multiple of 4; cin

@@ -55,24 +55,48 @@ def _bn_batch(v: Tensor, w: Tensor, b: Tensor, eps: float) -> Tensor:
     return F.batch_norm(v, None, None, w, b, training=True, eps=eps)
 
 
+def sync_batch_norm(group=None) -> Callable[[Tensor, Tensor, Tensor, float], Tensor]:
+    """SyncBN: BatchNorm with batch statistics over the clips of every rank of
+    ``group`` (the opt-in mode of the HIP cell).  Per-channel
+    sums and sums of squares are all-reduced with the differentiable
+    ``torch.distributed.nn`` all-reduce, so autograd gives the matching
+    backward (the all-reduced sum dy and sum dy * xhat of the HIP backward)."""
+    from torch.distributed.nn.functional import all_reduce
+
+    def bn(v: Tensor, w: Tensor, b: Tensor, eps: float) -> Tensor:
+        vd = v.double()                                  # fp64 sums: no cancellation in var
+        n = torch.tensor([float(v.shape[0] * v.shape[2] * v.shape[3])], dtype=torch.float64)
+        s1 = all_reduce(vd.sum((0, 2, 3)), group=group)
+        s2 = all_reduce((vd * vd).sum((0, 2, 3)), group=group)
+        cnt = all_reduce(n, group=group)
+        mean = s1 / cnt
+        var = s2 / cnt - mean * mean
+        xhat = (vd - mean[None, :, None, None]) / torch.sqrt(var + eps)[None, :, None, None]
+        return (xhat * w[None, :, None, None] + b[None, :, None, None]).to(v.dtype)
+    return bn
+
+
 def horizontal_frame(sd: Params, prefix: str, x_t: Tensor, inh: Tensor, exc: Tensor,
                      act: Callable[[Tensor], Tensor], *, no_inh: bool = False,
-                     hgru: bool = False, eps: float = 1e-3):
+                     hgru: bool = False, eps: float = 1e-3, bn=None):
     """One recurrent step.  Returns ``(inh_new, exc_new, att)``.
 
     InT ``rCell.forward`` (models/InT.py:145-179) with ``use_attention=True``
     (hard-wired by ``InT.__init__`` at models/InT.py:196); ``hgru=True`` gives
     ``hConvGRUCell.forward`` (models/ffhgru_hierarchy.py:135-173), whose only
     difference is that the gated inhibition is the attention map itself
-    (models/ffhgru_hierarchy.py:147).
+    (models/ffhgru_hierarchy.py:147).  ``bn``: the BatchNorm (default: batch
+    statistics of this process's clips, as the reference's DataParallel
+    replicas; :func:`sync_batch_norm` for SyncBN).
     """
+    bnf = bn or _bn_batch
     k = sd[f"{prefix}w_exc"].shape[-1]
     pad = k // 2
     att = torch.sigmoid(_gate(sd, prefix, "a_w", x_t) + _gate(sd, prefix, "a_u", exc))  # InT.py:148
     g_exc = att * exc                                                                   # InT.py:153
     g_inh = att if hgru else inh                                                        # InT.py:157 / ffhgru:147
     if not no_inh:
-        c_i = _bn_batch(F.conv2d(g_exc, sd[f"{prefix}w_inh"], padding=pad),
+        c_i = bnf(F.conv2d(g_exc, sd[f"{prefix}w_inh"], padding=pad),
                         sd[f"{prefix}bn.0.weight"], sd[f"{prefix}bn.0.bias"], eps)      # InT.py:161
         i_hat = act(x_t - act(c_i * (sd[f"{prefix}alpha"] * g_inh + sd[f"{prefix}mu"])))  # InT.py:162
         i_g = torch.sigmoid(_gate(sd, prefix, "i_w", x_t) + _gate(sd, prefix, "i_u", g_inh))  # InT.py:165
@@ -80,7 +104,7 @@ def horizontal_frame(sd: Params, prefix: str, x_t: Tensor, inh: Tensor, exc: Ten
     else:
         inh_new, g_inh = g_exc, exc                                                      # InT.py:168
     e_g = torch.sigmoid(_gate(sd, prefix, "e_w", g_inh) + _gate(sd, prefix, "e_u", g_exc))  # InT.py:171
-    c_e = _bn_batch(F.conv2d(inh_new, sd[f"{prefix}w_exc"], padding=pad),
+    c_e = bnf(F.conv2d(inh_new, sd[f"{prefix}w_exc"], padding=pad),
                     sd[f"{prefix}bn.1.weight"], sd[f"{prefix}bn.1.bias"], eps)            # InT.py:172
     e_hat = act(c_e * (sd[f"{prefix}kappa"] * inh_new + sd[f"{prefix}gamma"]))         # InT.py:173
     exc_new = (1 - e_g) * exc + e_g * e_hat                                              # InT.py:175
@@ -106,7 +130,7 @@ def readout(sd: Params, exc: Tensor, x: Tensor) -> Tensor:
 
 
 def recurrent_forward(sd: Params, x: Tensor, *, act: str = "softplus", no_inh: bool = False,
-                      hgru: bool = False, testmode: bool = False, eps: float = 1e-3):
+                      hgru: bool = False, testmode: bool = False, eps: float = 1e-3, bn=None):
     """Whole-clip forward of InT (models/InT.py:210-245) or FFhGRU
     (models/ffhgru_hierarchy.py:211-276).
 
@@ -122,7 +146,7 @@ def recurrent_forward(sd: Params, x: Tensor, *, act: str = "softplus", no_inh: b
     exc_seq, att_seq = [], []
     for t in range(t_len):                               # InT.py:223
         inh, exc, att = horizontal_frame(sd, "unit1.", xbn[:, :, t], inh, exc, nl,
-                                         no_inh=no_inh, hgru=hgru, eps=eps)
+                                         no_inh=no_inh, hgru=hgru, eps=eps, bn=bn)
         if testmode:
             exc_seq.append(exc)
             att_seq.append(att)

@@ -39,11 +39,100 @@ enum SmallSlot {
 constexpr int SLAB_G = 6 * 1024;                 // 6 gate weights [n][ci]
 constexpr int SLAB = SLAB_G + NSMALL * 32;
 constexpr int NTRANS = 12;                       // backward transients incl. dAt, GEfin
-// BatchNorm batch sums are fp64 atomics spread over NBNC copies (workgroup w
-// adds into copy w % NBNC; readers sum the copies): with one copy, all 256-1024
-// workgroups of a launch serialised on the same 64-96 addresses (measured
-// 7.5 us per forward conv launch, 5 us per k_pw_bb launch).
-constexpr int NBNC = 16;
+// BatchNorm batch sums, bitwise reproducible (no floating-point atomics):
+// every producer (forward: the conv workgroup of one clip / tile; backward: a
+// point-wise workgroup) stores its partial sums in its own slot; the last
+// producer to arrive in its group of bn_gsize() (an arrival ticket: stores
+// drained, agent-scope release, one relaxed agent-scope counter add, the last
+// arriver acquires) adds the group's partials in slot order and stores the
+// group sum; a consumer adds the <= NGRP group sums in group order.  Every
+// sum therefore has one fixed association, whatever the dispatch order or
+// the XCD placement: runs, and hipGraph replays, agree bit for bit.
+constexpr int NGRP = 16;
+constexpr int BNB_WG_PER_CLIP = 8;     // backward producers per clip at most (PW_PARTS)
+__host__ __device__ inline int bn_gsize(int nprod) { return (nprod + NGRP - 1) / NGRP; }
+__host__ __device__ inline int bn_ngrp(int nprod) {
+  const int g = bn_gsize(nprod);
+  return (nprod + g - 1) / g;
+}
+struct BnSlot {       // one (frame, BatchNorm) reduction
+  float* part;        // [nprod][64] per-producer partials
+  double* grp;        // [NGRP][NV] group sums (NV: 96 forward, 64 backward)
+  unsigned* cnt;      // [NGRP] arrival tickets, zeroed before every call
+  int nprod;          // producers in the launch
+};
+
+// Arrival ticket (all threads call it after storing their partials): every
+// wave drains its stores, one lane releases at agent scope and takes a ticket
+// with one relaxed agent-scope vector atomic; the group's last arriver
+// acquires (drops this CU's L1) and every thread of it gets true.  flag: an
+// LDS word no other code touches until the caller's next barrier.
+__device__ __forceinline__ bool bn_arrive(unsigned* cnt, int nmem, int tid, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(nmem - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// The last arriver of group g: sums of the group's partials in slot order, fp64.
+// Thread (v = tid & 63, q = tid >> 6) adds members q, q + Q, ...; the Q
+// quarter sums are then added in q order.  FWD: partial = (mean_b[32], M2_b[32])
+// -> grp = (sum mean_b, sum mean_b^2, sum M2_b); else grp = sum of the 64 values.
+// scr: NTH * (FWD ? 2 : 1) doubles of LDS.
+template <int NTH, bool FWD>
+__device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
+  constexpr int Q = NTH / 64;
+  const int G = bn_gsize(s.nprod), m0 = g * G, m1 = min(s.nprod, m0 + G);
+  const int v = tid & 63, q = tid >> 6;
+  double a = 0.0, b = 0.0;
+#pragma unroll 8
+  for (int m = m0 + q; m < m1; m += Q) {
+    const double x = (double)s.part[(size_t)m * 64 + v];
+    a += x;
+    b += x * x;
+  }
+  constexpr int W = FWD ? 2 : 1;
+  scr[W * tid] = a;
+  if (FWD) scr[W * tid + 1] = b;
+  __syncthreads();
+  if (tid < 64) {
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      sa += scr[W * (k * 64 + tid)];
+      if (FWD) sb += scr[W * (k * 64 + tid) + 1];
+    }
+    if (FWD) {
+      double* o = s.grp + (size_t)g * 96;
+      if (tid < 32) { o[tid] = sa; o[32 + tid] = sb; }
+      else o[32 + tid] = sa;                           // sum M2_b at 64 + (tid - 32)
+    } else {
+      s.grp[(size_t)g * 64 + tid] = sa;
+    }
+  }
+}
+
+// Producer side: this workgroup's 64 partial values (lanes tid < 64 hold
+// value tid) into slot `prod`, the ticket, and the group sum if last.
+template <int NTH, bool FWD>
+__device__ __forceinline__ void bn_publish(const BnSlot& s, int prod, float val, int tid, int* flag,
+                                           double* scr) {
+  if (tid < 64) s.part[(size_t)prod * 64 + tid] = val;
+  const int G = bn_gsize(s.nprod), g = prod / G;
+  const int nmem = min(G, s.nprod - g * G);
+  if (bn_arrive(s.cnt + g, nmem, tid, flag)) bn_group_sum<NTH, FWD>(s, g, tid, scr);
+}
 
 // ----------------------------------------------------------------- arguments
 template <class S>
@@ -83,19 +172,49 @@ struct CellArgs {
   S *I, *gE, *ci, *ce, *eg;
   S* at;                                // hGRU only: attention map per frame (the gated inhibition)
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
-  double* bnacc;                        // fwd BN sums [T][2][NBNC][3][32]: sum mean_b, sum mean_b^2, sum M2_b
+  // BatchNorm reductions (see BnSlot), slot (t, bn) = t * 2 + bn:
+  float* bnf_part;                      // fwd [T][2][B][64] per-clip (mean_b, M2_b)
+  double* bnf_grp;                      // fwd [T][2][NGRP][96] sum mean_b, sum mean_b^2, sum M2_b
+  unsigned* bnf_cnt;                    // fwd [T][2][NGRP] tickets
   float* gates;                         // [B][T][C][32][32] or null
   // backward transients, channels-last [B][32][32][32] in the storage type
   S *dEn, *dcE, *dIl, *dEp, *dcI, *GI, *dgEp, *dxp, *dgE, *dIt;
   S* dAt;                               // hGRU: d loss / d att_t through the gated inhibition
   const float* GEfin;                   // dE of the last frame (channels-last)
   S *dci_s, *dce_s;                     // [T][B][32][32][32] conv-output grads (for k_wgrad)
-  double* bnbacc;                       // bwd BN sums [T][2][NBNC][2][32]: sum dy, sum dy*xhat
+  float* bnb_part;                      // bwd [T][2][PW_PARTS B][64] per-workgroup (sum dy, sum dy*xhat)
+  double* bnb_grp;                      // bwd [T][2][NGRP][64]
+  unsigned* bnb_cnt;                    // bwd [T][2][NGRP]
+  // SyncBN (pt_cell_dist): the batch totals all-reduced over bn_world replicas,
+  // fwd [T][2][96] then bwd [T][2][64]; null = per-replica statistics
+  const double* bnsync;
+  int bn_world;                         // replicas sharing the statistics (1 = per replica)
   float* slab;                          // [B][PW_PARTS][SLAB]
   int conv_done;                        // k_pw_ba: dgE holds conv^T(w_inh) + dgEp
 };
 
 __device__ __forceinline__ size_t fr_off(int t, int B) { return (size_t)t * B * NPIX * C; }
+
+// (frame t, BatchNorm bn) reduction slots; nprod of the backward ones: the
+// launch's workgroups (k_pw_bb -> bn 0, k_pw_ba -> bn 1)
+template <class S>
+__host__ __device__ inline BnSlot bnf_slot(const CellArgs<S>& a, int t, int bn) {
+  const size_t k = (size_t)t * 2 + bn;
+  return {a.bnf_part + k * a.B * 64, a.bnf_grp + k * NGRP * 96, a.bnf_cnt + k * NGRP, a.B};
+}
+// what the forward consumers finalise: the group sums, or (SyncBN) the totals
+template <class S>
+__host__ __device__ inline const double* bnf_src(const CellArgs<S>& a, int t, int bn) {
+  return a.bnsync ? a.bnsync + ((size_t)t * 2 + bn) * 96 : a.bnf_grp + ((size_t)t * 2 + bn) * NGRP * 96;
+}
+template <class S>
+__host__ __device__ inline int bnf_nsrc(const CellArgs<S>& a) { return a.bnsync ? 1 : bn_ngrp(a.B); }
+template <class S>
+__host__ __device__ inline BnSlot bnb_slot(const CellArgs<S>& a, int t, int bn, int nprod) {
+  const size_t k = (size_t)t * 2 + bn;
+  return {a.bnb_part + k * (size_t)a.B * BNB_WG_PER_CLIP * 64, a.bnb_grp + k * NGRP * 64, a.bnb_cnt + k * NGRP,
+          nprod};
+}
 __device__ __forceinline__ size_t clip_off(int b) { return (size_t)b * NPIX * C; }
 
 // Spatial tiling.  A frame larger than 32x32 (H, W multiples of 32) is held as
@@ -215,19 +334,19 @@ __device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const St
   }
 }
 
-// Forward BN: batch mean / rstd per channel from the fp64 sums of per-clip
+// Forward BN: batch mean / rstd per channel (B = clips / tiles counted, all
+// replicas' under SyncBN) from the fp64 sums (ng group sums, added in order) of per-clip
 // (mean_b, mean_b^2, M2_b) (Chan et al.: M2 = sum M2_b + n (sum mean_b^2 -
 // (sum mean_b)^2 / B)); all threads end with them in stat[0..63].
 // Lanes fl < 32 of ONE wave finalise (the caller picks the wave; others pass
 // fl >= 32); stat is read only after the caller's next workgroup barrier.
-__device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps, float* stat,
-                                float* gstat, int fl) {
+__device__ void bn_fwd_finalize(const double* __restrict__ grp, int ng, int B, float eps,
+                                float* stat, float* gstat, int fl) {
   if (fl < 32) {
     const int tid = fl;
     double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-#pragma unroll
-    for (int k = 0; k < NBNC; ++k) {
-      s1 += acc[k * 96 + tid]; s2 += acc[k * 96 + 32 + tid]; s3 += acc[k * 96 + 64 + tid];
+    for (int k = 0; k < ng; ++k) {
+      s1 += grp[k * 96 + tid]; s2 += grp[k * 96 + 32 + tid]; s3 += grp[k * 96 + 64 + tid];
     }
     const double mean = s1 / B;
     double m2 = s3 + (double)NPIX * (s2 - s1 * s1 / B);
@@ -240,14 +359,14 @@ __device__ void bn_fwd_finalize(const double* __restrict__ acc, int B, float eps
   }
 }
 
-// Per-clip (mean, M2) of the conv outputs held in acc (PL layout), accumulated
-// into the fp64 batch sums.  Each wave runs a two-pass (mean, M2) over its own
+// Per-clip (mean, M2) of the conv outputs held in acc (PL layout), published
+// to the deterministic batch reduction (bn_publish; scr / flag: free LDS).  Each wave runs a two-pass (mean, M2) over its own
 // RW rows (its per-channel means go through its own LDS slot, no workgroup
 // barrier); one barrier, then Chan's combination over the NW equal-sized wave
 // blocks: M2 = sum M2_w + n_w sum (mean_w - mean)^2.  red: 2 * NW * 32 floats.
 template <int RW, int NW>
-__device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out, int lane,
-                               int wave, int tid, int ablate) {
+__device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, const BnSlot& out, int prod,
+                               int lane, int wave, int tid, int ablate, int* flag, double* scr) {
   const int h = lane >> 5;
   const int ch = pl_ch(pl_sum_reg(lane), h);
   f32x16 s = acc[0];
@@ -273,25 +392,22 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, double* out,
   const float tq = pl_lane_sum(q, lane);
   if (!(lane & 16)) red[NW * 32 + wave * 32 + ch] = tq;
   __syncthreads();
-  if (tid < 32 && !(ablate & 32768)) {
-    float mn = 0.f;
+  if (ablate & 32768) return;
+  // lanes 0-31: channel tid's block mean; lanes 32-63: its M2 (Chan over the NW wave blocks)
+  const int ch2 = tid & 31;
+  float mn = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) mn += red[w * 32 + tid];
-    mn *= 1.f / NW;
-    float v = 0.f, dv = 0.f;
+  for (int w = 0; w < NW; ++w) mn += red[w * 32 + ch2];
+  mn *= 1.f / NW;
+  float v = 0.f, dv = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const float d = red[w * 32 + tid] - mn;
-      v += red[NW * 32 + w * 32 + tid];
-      dv += d * d;
-    }
-    v += dv * (float)(RW * IMG);
-    const double md = (double)mn;
-    out += (blockIdx.x % NBNC) * 96;
-    unsafeAtomicAdd(out + tid, md);
-    unsafeAtomicAdd(out + 32 + tid, md * md);
-    unsafeAtomicAdd(out + 64 + tid, (double)v);
+  for (int w = 0; w < NW; ++w) {
+    const float d = red[w * 32 + ch2] - mn;
+    v += red[NW * 32 + w * 32 + ch2];
+    dv += d * d;
   }
+  v += dv * (float)(RW * IMG);
+  bn_publish<NW * 64, true>(out, prod, tid < 32 ? mn : v, tid, flag, scr);
 }
 
 // =========================================================================
@@ -318,12 +434,14 @@ struct ConvArgs {
   const S* dc;                  // FILL_BNBWD: dy
   const S* raw;                 // FILL_BNBWD: pre-BN conv output of the forward
   const float* bnstat;          // FILL_BNBWD: mean[32], rstd[32]
-  const double* bnb;            // FILL_BNBWD: sum dy[32], sum dy*xhat[32]
+  const double* bnb;            // FILL_BNBWD: group sums [ngrp][64] (sum dy[32], sum dy*xhat[32])
+  int bnb_ngrp;
+  int bnB;                      // FILL_BNBWD: clips / tiles in the statistics (all replicas' under SyncBN)
   const float* bnw;             // FILL_BNBWD: BN gamma
   S* fill_out;                  // FILL_BNBWD: dx written here too
   const F* wf;
   S* out_raw;                   // EPI_FWD
-  double* bnacc;                // EPI_FWD
+  BnSlot bnout;                 // EPI_FWD: per-clip BN partials
   S* out;                       // EPI_ADD
   const S *add0, *add1;         // EPI_ADD (add1 may be null)
 };
@@ -409,10 +527,9 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
   if constexpr (FILL == FILL_BNBWD) {
     if (tid < 32) {
       // dx = A dy + Bc raw + Cc  with A = rstd g, xhat = (raw - mean) rstd
-      const double inv = 1.0 / ((double)a.B * NPIX);
+      const double inv = 1.0 / ((double)a.bnB * NPIX);
       double sd = 0.0, sdx = 0.0;
-#pragma unroll
-      for (int k = 0; k < NBNC; ++k) { sd += a.bnb[k * 64 + tid]; sdx += a.bnb[k * 64 + 32 + tid]; }
+      for (int k = 0; k < a.bnb_ngrp; ++k) { sd += a.bnb[k * 64 + tid]; sdx += a.bnb[k * 64 + 32 + tid]; }
       const float md = (float)(sd * inv), mdx = (float)(sdx * inv);
       const float mean = a.bnstat[tid], rstd = a.bnstat[32 + tid];
       const float A = rstd * a.bnw[tid];
@@ -504,7 +621,10 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RW) * IMG + px) * C, h};
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate, sr);
       if (a.ablate & 256) return;
-      if (!(a.ablate & 8)) bn_fwd_partial<RW, NW>(acc, red, a.bnacc, lane, wave, tid, a.ablate);
+      // the tile is free once every wave has passed bn_fwd_partial's barrier
+      if (!(a.ablate & 8))
+        bn_fwd_partial<RW, NW>(acc, red, a.bnout, b, lane, wave, tid, a.ablate,
+                               (int*)(smem + NTH * 16), (double*)smem);
     } else if constexpr (sizeof(S) == 2) {
       bf16x4 p0[RW][4], p1[RW][4];
       const AddRowBf16<RW> ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
@@ -525,6 +645,16 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
     }
   }
 }
+// SyncBN: the ngrp group sums of one reduction, added in group order, into the
+// buffer the replicas all-reduce (pt_cell_dist.bn_buf).
+__global__ void k_bn_total(const double* __restrict__ grp, int ngrp, int nv, double* __restrict__ out) {
+  const int v = threadIdx.x;
+  if (v >= nv) return;
+  double s = 0.0;
+  for (int k = 0; k < ngrp; ++k) s += grp[k * nv + v];
+  out[v] = s;
+}
+
 // Distinct kernel names per role (rocprof summaries tell them apart).
 template <class S, int PAD, int NTH = NT>
 __global__ __launch_bounds__(NTH, 1) void k_conv_fwd(ConvArgs<S> a) {     // conv + BN partials
@@ -568,6 +698,7 @@ constexpr int PWF_WGPC = IMG / (PW_NW * PWF_RPP);  // workgroups per clip (8)
 constexpr int PWA_WGPC = IMG / (PW_NW * PWA_RPP);  // (2)
 constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (8)
 constexpr int PW_PARTS = PWB_WGPC > PWA_WGPC ? PWB_WGPC : PWA_WGPC;   // slab partitions per clip
+static_assert(PW_PARTS <= BNB_WG_PER_CLIP, "backward BN partial slots per clip");
 
 constexpr int PW_NGACC = 4;   // 1x1 weight-gradient tiles accumulated in LDS per workgroup
 template <int RPP, bool BWD>
@@ -745,21 +876,22 @@ __device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, c
   __syncthreads();
 }
 
-// Workgroup totals of two per-lane channel sums -> fp64 batch sums.
-__device__ void bn_bwd_partial(float s0, float s1, float* red, double* out, int lane, int wave,
-                               int tid) {
+// Workgroup totals of two per-lane channel sums -> the deterministic batch
+// reduction (bn_publish).  red: 512 floats (reused as the group-sum scratch);
+// flag: an LDS word outside red.
+__device__ void bn_bwd_partial(float s0, float s1, float* red, const BnSlot& out, int lane,
+                               int wave, int tid, int* flag) {
   s0 += __shfl_xor(s0, 32);
   s1 += __shfl_xor(s1, 32);
   if (lane < 32) { red[wave * 32 + lane] = s0; red[256 + wave * 32 + lane] = s1; }
   __syncthreads();
-  if (tid < 32) {
-    float a = 0.f, b = 0.f;
+  float a = 0.f;                        // lanes 0-31: sum dy; 32-63: sum dy * xhat
+  if (tid < 64) {
+    const int o = tid < 32 ? tid : 256 + tid - 32;
 #pragma unroll
-    for (int w = 0; w < PW_NW; ++w) { a += red[w * 32 + tid]; b += red[256 + w * 32 + tid]; }
-    out += (blockIdx.x % NBNC) * 64;
-    unsafeAtomicAdd(out + tid, (double)a);
-    unsafeAtomicAdd(out + 32 + tid, (double)b);
+    for (int w = 0; w < PW_NW; ++w) a += red[o + w * 32];
   }
+  bn_publish<PW_NT, false>(out, blockIdx.x, a, tid, flag, (double*)red);
   __syncthreads();
 }
 
@@ -882,7 +1014,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   // (and the barrier below for it); the other waves' row tiles go out first.
   const bool finw = wave == PW_NW - 1;
   if (finw && t > 0 && !(a.ablate & 65536))
-    bn_fwd_finalize(a.bnacc + ((size_t)(t - 1) * 2 + 1) * NBNC * 96, B, a.eps, L.stat + 64,
+    bn_fwd_finalize(bnf_src(a, t - 1, 1), bnf_nsrc(a), B * a.bn_world, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   const FaIn<S> in = fa_load(a, ro, c, h);
   if (t < T && !(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
@@ -974,7 +1106,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   const FbIn<S> in = fb_load<S, HG>(a, ro, c, h);
   stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   // (finalising first in a separate wave, as k_pw_fa does, measured no gain here)
-  bn_fwd_finalize(a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96, B, a.eps, L.stat,
+  bn_fwd_finalize(bnf_src(a, t, 0), bnf_nsrc(a), B * a.bn_world, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
@@ -1110,7 +1242,8 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
-  if (head && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64, lane, wave, tid);
+  if (head && !(a.ablate & 8))   // L.stat is unused by the backward kernels: the ticket's flag word
+    bn_bwd_partial(bs0, bs1, L.red, bnb_slot(a, t, 1, B * PWA_WGPC), lane, wave, tid, (int*)L.stat);
   if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
   if (tail && (head || HG) && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
 }
@@ -1310,7 +1443,8 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   }
   sm[4] = bs1;
   sm[5] = bs0;
-  if (!a.no_inh && !(a.ablate & 8)) bn_bwd_partial(bs0, bs1, L.red, a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64, lane, wave, tid);
+  if (!a.no_inh && !(a.ablate & 8))
+    bn_bwd_partial(bs0, bs1, L.red, bnb_slot(a, t, 0, B * PWB_WGPC), lane, wave, tid, (int*)L.stat);
   if (a.ablate & 32) return;
   flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5 (bf16: written by gate_wgrad)
@@ -1756,6 +1890,7 @@ __global__ void k_prep(PrepArgs<S> p) {
 // ---------------------------------------------------------------- reductions
 struct ReduceArgs {
   int B, K, nwg;
+  int part;             // 0: the per-clip slabs (all but the k x k weights); 1: the k x k weights
   int Cu;               // the caller's channel count (<= 32); padded channels are dropped
   const float* slab;    // [rows][SLAB]
   const float* wslab;   // [2][nwg][K*K][1024]
@@ -1786,8 +1921,8 @@ __global__ void k_reduce(ReduceArgs r) {
   const int KK = r.K * r.K;
   const int n_small = SLAB;                  // slab entries
   const int n_w = 2 * KK * 1024;             // conv weights
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n_small + n_w;
-       e += gridDim.x * blockDim.x) {
+  const int e0 = r.part == 0 ? 0 : n_small, e1 = r.part == 0 ? n_small : n_small + n_w;
+  for (int e = e0 + blockIdx.x * blockDim.x + threadIdx.x; e < e1; e += gridDim.x * blockDim.x) {
     if (e < n_small) {
       const float s = strided_sum(r.slab + e, SLAB, r.B);
       if (e < SLAB_G) {
@@ -2007,7 +2142,9 @@ struct Plan {
   // saved offsets
   size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], o_pad, saved;
   // workspace offsets
-  size_t o_bnacc, o_bnbacc, o_tr[NTRANS], o_dci, o_dce, o_slab, o_wslab, ws;
+  size_t o_bnf_cnt, o_bnf_part, o_bnf_grp, o_bnb_cnt, o_bnb_part, o_bnb_grp;   // BnSlot storage
+  size_t bnf_cnt_bytes, bnb_cnt_bytes;
+  size_t o_tr[NTRANS], o_dci, o_dce, o_slab, o_wslab, ws;
   int nwg;
 };
 
@@ -2053,8 +2190,15 @@ Plan plan(const pt_cell_desc* d) {
   p.o_pad = o; o += p.Cu < C ? al(pad_layout(p.K * p.K).total * 4) : 0;
   p.saved = o;
   o = 0;
-  p.o_bnacc = o; o += al((size_t)p.T * 2 * NBNC * 96 * 8);
-  p.o_bnbacc = o; o += al((size_t)p.T * 2 * NBNC * 64 * 8);
+  // tickets first (the only words cleared per call), then partials and group sums
+  p.bnf_cnt_bytes = al((size_t)p.T * 2 * NGRP * 4);
+  p.o_bnf_cnt = o; o += p.bnf_cnt_bytes;
+  p.o_bnf_part = o; o += al((size_t)p.T * 2 * p.B * 64 * 4);
+  p.o_bnf_grp = o; o += al((size_t)p.T * 2 * NGRP * 96 * 8);
+  p.bnb_cnt_bytes = al((size_t)p.T * 2 * NGRP * 4);
+  p.o_bnb_cnt = o; o += p.bnb_cnt_bytes;
+  p.o_bnb_part = o; o += al((size_t)p.T * 2 * p.B * BNB_WG_PER_CLIP * 64 * 4);
+  p.o_bnb_grp = o; o += al((size_t)p.T * 2 * NGRP * 64 * 8);
   for (int i = 0; i < NTRANS; ++i) { p.o_tr[i] = o; o += al(p.frame * 4); }   // GEfin f32
   p.o_dci = o; o += fbytes;
   p.o_dce = o; o += fbytes;
@@ -2074,6 +2218,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   a.Cu = p.Cu;
   a.ntx = p.ntx; a.nty = p.nty;
   a.hgru = d->cell == PT_CELL_HGRU;
+  a.bn_world = 1;
   a.x = x;
   a.xu8 = d->x_format == PT_X_U8_NTHWC;
   {
@@ -2095,8 +2240,12 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   a.at = a.hgru ? (S*)(saved + p.o_at) : nullptr;
   a.bnstat = (float*)(saved + p.o_bnstat);
   if (ws) {
-    a.bnacc = (double*)(ws + p.o_bnacc);
-    a.bnbacc = (double*)(ws + p.o_bnbacc);
+    a.bnf_cnt = (unsigned*)(ws + p.o_bnf_cnt);
+    a.bnf_part = (float*)(ws + p.o_bnf_part);
+    a.bnf_grp = (double*)(ws + p.o_bnf_grp);
+    a.bnb_cnt = (unsigned*)(ws + p.o_bnb_cnt);
+    a.bnb_part = (float*)(ws + p.o_bnb_part);
+    a.bnb_grp = (double*)(ws + p.o_bnb_grp);
     S** tr[NTRANS] = {&a.dEn, &a.dcE, &a.dIl, &a.dEp, &a.dcI, &a.GI, &a.dgEp, &a.dxp,
                       &a.dgE, &a.dIt, &a.dAt, nullptr};
     for (int i = 0; i < NTRANS - 1; ++i) *tr[i] = (S*)(ws + p.o_tr[i]);
@@ -2180,13 +2329,33 @@ ConvArgs<S> conv_args(const CellArgs<S>& a) {
   ConvArgs<S> c;
   memset(&c, 0, sizeof(c));
   c.B = a.B; c.K = a.K; c.ablate = a.ablate;
+  c.bnB = a.B * a.bn_world;
   c.ntx = a.ntx; c.nty = a.nty;
   return c;
 }
 
+// SyncBN step after a BatchNorm producer launch: the group sums of reduction
+// `slot` added into bn_buf + off, then the caller's all-reduce of those nv
+// doubles, enqueued on the same stream.
+int bn_sync(const pt_cell_dist* dist, const double* grp, int ngrp, int nv, size_t off, hipStream_t st) {
+  hipLaunchKernelGGL(k_bn_total, dim3(1), dim3(128), 0, st, grp, ngrp, nv, dist->bn_buf + off);
+  HIPCHK(hipGetLastError());
+  if (dist->allreduce(dist->user, (int64_t)off, (int64_t)nv) != 0)
+    return fail(PT_ERR_ARG, "BatchNorm all-reduce callback failed%s%ld");
+  return 0;
+}
+inline bool syncbn(const pt_cell_dist* dist) { return dist && dist->bn_world > 1; }
+int check_dist(const pt_cell_dist* dist) {
+  if (!dist) return 0;
+  if (dist->bn_world < 1) return fail(PT_ERR_ARG, "bn_world must be >= 1%s (got %ld)", "", dist->bn_world);
+  if (dist->bn_world > 1 && (!dist->bn_buf || !dist->allreduce))
+    return fail(PT_ERR_ARG, "SyncBN (bn_world > 1) needs bn_buf and allreduce%s%ld");
+  return 0;
+}
+
 template <class S>
 int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, void* saved,
-                void* ws, float* e_last, float* gates, hipStream_t st) {
+                void* ws, float* e_last, float* gates, const pt_cell_dist* dist, hipStream_t st) {
   const Plan p = plan(d);
   if (int rc = set_lds_attrs<S>()) return rc;
   pt_cell_params padded;
@@ -2199,6 +2368,7 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
   a.gates = gates;
+  if (syncbn(dist)) { a.bnsync = dist->bn_buf; a.bn_world = dist->bn_world; }
   PrepArgs<S> pa{};
   pa.K = p.K; pa.w_inh = d->no_inh ? nullptr : pr->w_inh; pa.w_exc = pr->w_exc;
   for (int i = 0; i < 6; ++i) {
@@ -2208,7 +2378,7 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   }
   pa.wf_inh = (S*)((char*)saved + p.o_wf[0]); pa.wf_exc = (S*)((char*)saved + p.o_wf[1]);
   pa.wt_inh = (S*)((char*)saved + p.o_wf[2]); pa.wt_exc = (S*)((char*)saved + p.o_wf[3]);
-  HIPCHK(zero_async((char*)ws + p.o_bnacc, (size_t)p.T * 2 * NBNC * 96 * 8, st));
+  HIPCHK(zero_async((char*)ws + p.o_bnf_cnt, p.bnf_cnt_bytes, st));     // BN tickets
   timed(PT_K_PREP, st, [&] { hipLaunchKernelGGL(k_prep<S>, dim3(256), dim3(256), 0, st, pa); });
   const dim3 gpf(p.B * PWF_WGPC);
   const size_t lpf = (pw_lds_bytes<PWF_RPP, false>());
@@ -2221,14 +2391,18 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
     timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });
     if (t == p.T) break;
     if (!d->no_inh) {
-      ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnacc = a.bnacc + ((size_t)t * 2 + 0) * NBNC * 96;
+      ca.src = a.gE + t * fs; ca.out_raw = a.ci + t * fs; ca.bnout = bnf_slot(a, t, 0);
       timed(PT_K_CONV_FA, st, [&] {
         launch_conv_fwd<S>(p, st, ca); });
+      if (syncbn(dist))
+        if (int rc = bn_sync(dist, ca.bnout.grp, bn_ngrp(p.B), 96, ((size_t)t * 2 + 0) * 96, st)) return rc;
     }
     timed(PT_K_PW_FB, st, [&] { PW_LAUNCH(k_pw_fb, gpf, lpf); });
-    cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnacc = a.bnacc + ((size_t)t * 2 + 1) * NBNC * 96;
+    cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnout = bnf_slot(a, t, 1);
     timed(PT_K_CONV_FB, st, [&] {
       launch_conv_fwd<S>(p, st, cb); });
+    if (syncbn(dist))
+      if (int rc = bn_sync(dist, cb.bnout.grp, bn_ngrp(p.B), 96, ((size_t)t * 2 + 1) * 96, st)) return rc;
   }
   if (e_last)
     hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, st,
@@ -2238,10 +2412,14 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   return 0;
 }
 
+// The backward in two phases: 0 = the BPTT sweep and every gradient except
+// the two k x k weights (k_reduce part 0); 1 = k_wgrad and those two (part 1).
+// pt_cell_dist.grads_early_event is recorded between them, so the caller can
+// all-reduce the early gradients on another stream while k_wgrad runs.
 template <class S>
 int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
                  const void* saved, void* ws, const float* d_e_last, const pt_cell_grads* g,
-                 hipStream_t st) {
+                 const pt_cell_dist* dist, int phase, hipStream_t st) {
   const Plan p = plan(d);
   if (int rc = set_lds_attrs<S>()) return rc;
   pt_cell_params padded;
@@ -2251,8 +2429,38 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   }
   CellArgs<S> a;
   fill_args<S>(a, d, p, x, pr, (char*)saved, (char*)ws);
+  const bool sync = syncbn(dist);
+  if (sync) { a.bnsync = dist->bn_buf; a.bn_world = dist->bn_world; }
+  ReduceArgs r;
+  r.B = p.B * PW_PARTS; r.K = p.K; r.nwg = p.nwg;
+  r.slab = (const float*)((char*)ws + p.o_slab);
+  r.wslab = (const float*)((char*)ws + p.o_wslab);
+  r.g = *g;
+  r.Cu = p.Cu;
+  if (d->no_inh) { r.g.w_inh = nullptr; r.g.alpha = nullptr; r.g.mu = nullptr;
+                   r.g.bn_w[0] = nullptr; r.g.bn_b[0] = nullptr;
+                   r.g.gate_w[2] = r.g.gate_w[3] = nullptr; r.g.gate_b[2] = r.g.gate_b[3] = nullptr; }
+  if (phase == 1) {
+    float* wslab = (float*)((char*)ws + p.o_wslab);
+    const int conv0 = d->no_inh ? 1 : 0;
+    if (d->no_inh) HIPCHK(zero_async(wslab, (size_t)p.nwg * p.K * p.K * 1024 * 4, st));
+    timed(PT_K_WGRAD, st, [&] {
+      const dim3 grid(p.nwg, 2 - conv0, wgrad_groups(p.K, sizeof(S) == 2));
+      if (p.K <= 2 * PADMAX + 1)
+        hipLaunchKernelGGL((k_wgrad<S, PADMAX>), grid, dim3(wgrad_nt<S, PADMAX>()), (wgrad_lds_bytes<S, PADMAX>()), st, a,
+                           wslab, p.nwg, conv0);
+      else
+        hipLaunchKernelGGL((k_wgrad<S, PADBIG>), grid, dim3(NT), (wgrad_lds_bytes<S, PADBIG>()), st, a,
+                           wslab, p.nwg, conv0); });
+    r.part = 1;
+    const int n_w = 2 * p.K * p.K * 1024;                     // one thread per output element
+    timed(PT_K_REDUCE, st, [&] {
+      hipLaunchKernelGGL(k_reduce, dim3((n_w + 255) / 256), dim3(256), 0, st, r); });
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   HIPCHK(zero_async((char*)ws + p.o_slab, (size_t)p.B * PW_PARTS * SLAB * 4, st));
-  HIPCHK(zero_async((char*)ws + p.o_bnbacc, (size_t)p.T * 2 * NBNC * 64 * 8, st));
+  HIPCHK(zero_async((char*)ws + p.o_bnb_cnt, p.bnb_cnt_bytes, st));     // BN tickets
   hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty, p.Cu);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
@@ -2260,14 +2468,27 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   const size_t lcv = conv_lds_bytes<S>();
   const size_t fs = p.frame;
   const float* bst = a.bnstat;
+  const size_t sync_b = (size_t)p.T * 2 * 96;     // backward totals in bn_buf
+  // SyncBN: the backward sums of reduction (t, bn) all-reduced after their producer
+  auto sync_bwd = [&](int t, int bn, int nprod) {
+    return sync ? bn_sync(dist, bnb_slot(a, t, bn, nprod).grp, bn_ngrp(nprod), 64,
+                          sync_b + ((size_t)t * 2 + bn) * 64, st)
+                : 0;
+  };
+  auto bwd_src = [&](ConvArgs<S>& c, int t, int bn, int nprod) {
+    c.bnb = sync ? dist->bn_buf + sync_b + ((size_t)t * 2 + bn) * 64 : bnb_slot(a, t, bn, nprod).grp;
+    c.bnb_ngrp = sync ? 1 : bn_ngrp(nprod);
+  };
   a.t = p.T - 1;
   a.conv_done = 0;
   timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+  if (int rc = sync_bwd(p.T - 1, 1, p.B * PWA_WGPC)) return rc;
   for (int t = p.T - 1; t >= 0; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
     cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
-    cb.bnb = a.bnbacc + ((size_t)t * 2 + 1) * NBNC * 64; cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
+    bwd_src(cb, t, 1, p.B * PWA_WGPC);
+    cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
     cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
     timed(PT_K_CONV_BB, st, [&] {
       launch_conv_bwd<S>(p, st, cb); });
@@ -2275,10 +2496,12 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
     timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
     a.conv_done = 0;
     if (!d->no_inh) {
+      if (int rc = sync_bwd(t, 0, p.B * PWB_WGPC)) return rc;
       // dgE_t = conv^T(BN0-bwd(dcI), w_inh) + e_u^T d_e_pre ; frame 0's conv^T is dead (E_{-1}=0)
       ConvArgs<S> ca = conv_args(a);
       ca.dc = a.dcI; ca.raw = a.ci + t * fs; ca.bnstat = bst + (size_t)t * 128;
-      ca.bnb = a.bnbacc + ((size_t)t * 2 + 0) * NBNC * 64; ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
+      bwd_src(ca, t, 0, p.B * PWB_WGPC);
+      ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
       ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
       if (t >= 1) {
         timed(PT_K_CONV_BA, st, [&] {
@@ -2291,30 +2514,12 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
     }
     a.t = t - 1;
     timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+    if (t >= 1)
+      if (int rc = sync_bwd(t - 1, 1, p.B * PWA_WGPC)) return rc;
   }
-  float* wslab = (float*)((char*)ws + p.o_wslab);
-  const int conv0 = d->no_inh ? 1 : 0;
-  if (d->no_inh) HIPCHK(zero_async(wslab, (size_t)p.nwg * p.K * p.K * 1024 * 4, st));
-  timed(PT_K_WGRAD, st, [&] {
-    const dim3 grid(p.nwg, 2 - conv0, wgrad_groups(p.K, sizeof(S) == 2));
-    if (p.K <= 2 * PADMAX + 1)
-      hipLaunchKernelGGL((k_wgrad<S, PADMAX>), grid, dim3(wgrad_nt<S, PADMAX>()), (wgrad_lds_bytes<S, PADMAX>()), st, a,
-                         wslab, p.nwg, conv0);
-    else
-      hipLaunchKernelGGL((k_wgrad<S, PADBIG>), grid, dim3(NT), (wgrad_lds_bytes<S, PADBIG>()), st, a,
-                         wslab, p.nwg, conv0); });
-  ReduceArgs r;
-  r.B = p.B * PW_PARTS; r.K = p.K; r.nwg = p.nwg;
-  r.slab = (const float*)((char*)ws + p.o_slab);
-  r.wslab = wslab;
-  r.g = *g;
-  r.Cu = p.Cu;
-  if (d->no_inh) { r.g.w_inh = nullptr; r.g.alpha = nullptr; r.g.mu = nullptr;
-                   r.g.bn_w[0] = nullptr; r.g.bn_b[0] = nullptr;
-                   r.g.gate_w[2] = r.g.gate_w[3] = nullptr; r.g.gate_b[2] = r.g.gate_b[3] = nullptr; }
-  const int n_red = SLAB + 2 * p.K * p.K * 1024;              // one thread per output element
+  r.part = 0;
   timed(PT_K_REDUCE, st, [&] {
-    hipLaunchKernelGGL(k_reduce, dim3((n_red + 255) / 256), dim3(256), 0, st, r); });
+    hipLaunchKernelGGL(k_reduce, dim3((SLAB + 255) / 256), dim3(256), 0, st, r); });
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -2343,21 +2548,34 @@ size_t pt_cell_workspace_bytes(const pt_cell_desc* d) {
   return plan(d).ws;
 }
 
-int pt_cell_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* p, void* saved,
-                    void* ws, float* e_last, float* gates, pt_stream_t stream) {
+size_t pt_cell_bn_sync_doubles(const pt_cell_desc* d) {
+  if (check(d)) return 0;
+  return (size_t)d->frames * 2 * (96 + 64);
+}
+
+int pt_cell_forward_dist(const pt_cell_desc* d, const void* x, const pt_cell_params* p, void* saved,
+                         void* ws, float* e_last, float* gates, const pt_cell_dist* dist,
+                         pt_stream_t stream) {
   if (int rc = check(d)) return rc;
   if (!x || !p || !saved || !ws) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
+  if (int rc = check_dist(dist)) return rc;
   hipStream_t st = (hipStream_t)stream;
   const bool bf = d->dtype == PT_DTYPE_BF16;
   auto body = [&](hipStream_t s) {
-    return bf ? run_forward<bf16_t>(d, x, p, saved, ws, e_last, gates, s)
-              : run_forward<float>(d, x, p, saved, ws, e_last, gates, s);
+    return bf ? run_forward<bf16_t>(d, x, p, saved, ws, e_last, gates, dist, s)
+              : run_forward<float>(d, x, p, saved, ws, e_last, gates, dist, s);
   };
-  if (!use_graph()) return body(st);
+  // SyncBN calls back into the caller between launches: direct launches only
+  if (!use_graph() || syncbn(dist)) return body(st);
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
   k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
+}
+
+int pt_cell_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* p, void* saved,
+                    void* ws, float* e_last, float* gates, pt_stream_t stream) {
+  return pt_cell_forward_dist(d, x, p, saved, ws, e_last, gates, nullptr, stream);
 }
 
 int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, pt_stream_t stream) {
@@ -2373,22 +2591,39 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, p
   return 0;
 }
 
+int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_params* p,
+                          const void* saved, void* ws, const float* d_e_last,
+                          const pt_cell_grads* g, const pt_cell_dist* dist, pt_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  if (!x || !p || !saved || !ws || !d_e_last || !g) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
+  if (int rc = check_dist(dist)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const bool bf = d->dtype == PT_DTYPE_BF16;
+  const hipEvent_t early = dist ? (hipEvent_t)dist->grads_early_event : nullptr;
+  for (int phase = 0; phase < 2; ++phase) {
+    auto body = [&](hipStream_t s) {
+      return bf ? run_backward<bf16_t>(d, x, p, saved, ws, d_e_last, g, dist, phase, s)
+                : run_backward<float>(d, x, p, saved, ws, d_e_last, g, dist, phase, s);
+    };
+    int rc;
+    if (!use_graph() || syncbn(dist)) {
+      rc = body(st);
+    } else {
+      if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
+      ptg::Key k;
+      k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env());
+      rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
+    }
+    if (rc) return rc;
+    if (phase == 0 && early) HIPCHK(hipEventRecord(early, st));
+  }
+  return 0;
+}
+
 int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* p,
                      const void* saved, void* ws, const float* d_e_last, const pt_cell_grads* g,
                      pt_stream_t stream) {
-  if (int rc = check(d)) return rc;
-  if (!x || !p || !saved || !ws || !d_e_last || !g) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
-  hipStream_t st = (hipStream_t)stream;
-  const bool bf = d->dtype == PT_DTYPE_BF16;
-  auto body = [&](hipStream_t s) {
-    return bf ? run_backward<bf16_t>(d, x, p, saved, ws, d_e_last, g, s)
-              : run_backward<float>(d, x, p, saved, ws, d_e_last, g, s);
-  };
-  if (!use_graph()) return body(st);
-  if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
-  ptg::Key k;
-  k.add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env());
-  return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
+  return pt_cell_backward_dist(d, x, p, saved, ws, d_e_last, g, nullptr, stream);
 }
 
 int pt_cell_timing_enable(uint32_t kind_mask) {

@@ -264,6 +264,7 @@ __global__ void k_lpw_bwd(const float* __restrict__ dh, float* __restrict__ dc,
   }
   st4(dc + pc0, dcp);
   st4(dP + pg0, di); st4(dP + pg0 + 32, df); st4(dP + pg0 + 64, dg); st4(dP + pg0 + 96, dq);
+  if (!dPsum) return;      // per-step input: the sums over steps are formed from dP itself
   f32x4 s0 = di, s1 = df, s2 = dg, s3 = dq;
   if (!first) {
     s0 += ld4(dPsum + pg0); s1 += ld4(dPsum + pg0 + 32);
@@ -513,16 +514,19 @@ __global__ __launch_bounds__(NT, 1) void k_lwgrad(LWgradArgs a) {
 
 // ------------------------------------------------------------- reductions
 // Column sums of dPsum [npix][128] -> partial [nb][128] (bias gradients).
-__global__ void k_lcolsum(const float* __restrict__ src, float* __restrict__ part, int npix) {
+// Column sums of [npix][GC] rows (the bias gradients); per-step input: the
+// rows of every step's dP_t (npix = T * B * NPIX), read in S.
+template <class S>
+__global__ void k_lcolsum(const S* __restrict__ src, float* __restrict__ part, int npix) {
   const int c = threadIdx.x & 127, r0 = threadIdx.x >> 7;     // 256 threads: 2 row lanes
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int step = gridDim.x * 2;
   int r = blockIdx.x * 2 + r0;
   for (; r + 7 * step < npix; r += 8 * step) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += src[(size_t)(r + j * step) * GC + c];
+    for (int j = 0; j < 8; ++j) s[j] += ldf(src + (size_t)(r + j * step) * GC + c);
   }
-  for (; r < npix; r += step) s[0] += src[(size_t)r * GC + c];
+  for (; r < npix; r += step) s[0] += ldf(src + (size_t)r * GC + c);
   float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __shared__ float red[256];
   red[threadIdx.x] = t;
@@ -583,6 +587,30 @@ __global__ void k_to_cl(const float* __restrict__ src, S* __restrict__ dst, int 
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int c = e % HC, pix = (e / HC) % NPIX, b = e / (HC * NPIX);
     dst[e] = (S)(c < nc ? src[(((size_t)b * nc + c) * tn + t) * NPIX + pix] : 0.f);
+  }
+}
+// All steps at once: [B][nc][T][NPIX] fp32 <-> [T][B][NPIX][32] channels-last
+// (per-step inputs and their gradients; the per-step hidden states).
+template <class S>
+__global__ void k_to_cl_seq(const float* __restrict__ src, S* __restrict__ dst, int B, int nc, int T) {
+  const size_t n = (size_t)T * B * NPIX * HC;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % HC), pix = (int)((e / HC) % NPIX);
+    const size_t tb = e / ((size_t)HC * NPIX);
+    const int b = (int)(tb % B), t = (int)(tb / B);
+    dst[e] = (S)(c < nc ? src[(((size_t)b * nc + c) * T + t) * NPIX + pix] : 0.f);
+  }
+}
+template <class S>
+__global__ void k_from_cl_seq(const S* __restrict__ src, float* __restrict__ dst, int B, int nc, int T) {
+  const size_t n = (size_t)B * nc * T * NPIX;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int pix = (int)(e % NPIX), t = (int)((e / NPIX) % T);
+    const size_t bc = e / ((size_t)NPIX * T);
+    const int c = (int)(bc % nc), b = (int)(bc / nc);
+    dst[e] = ldf(src + (((size_t)t * B + b) * NPIX + pix) * HC + c);
   }
 }
 template <class S>
@@ -792,7 +820,7 @@ struct LPlan {
   // saved
   size_t o_fr[4], o_bias, o_x, o_xg, o_h0, o_c0, o_P, o_h, o_c, saved;
   // workspace
-  size_t o_dh, o_dc, o_dP, o_dPsum, o_dPsumS, o_jvP, o_wsh, o_wsx, o_col, ws;
+  size_t o_dh, o_dc, o_dP, o_dPsum, o_dPsumS, o_jvP, o_wsh, o_wsx, o_col, o_dx, ws;
 };
 
 int check(const pt_lstm_desc* d) {
@@ -829,7 +857,9 @@ LPlan plan(const pt_lstm_desc* d) {
   p.o_bias = o; o += al(GC * 4);
   p.xseq = d->x_seq != 0;
   p.o_x = o; o += al(p.npix * HC * p.es * (p.xseq ? p.T : 1));   // [steps][B][NPIX][32]
-  p.o_xg = o; o += al(p.npix * GC * 4);
+  // static x with a given h0: xg = Wx*x + b kept apart from P_0 (per-step
+  // input: P_t = Wx*x_t + b is written into P directly, no xg)
+  p.o_xg = o; o += p.xseq ? 0 : al(p.npix * GC * 4);
   p.o_h0 = o; o += al(p.npix * HC * p.es);
   p.o_c0 = o; o += al(p.npix * HC * 4);
   p.o_P = o; o += al(p.npix * GC * 4 * p.T);
@@ -843,12 +873,16 @@ LPlan plan(const pt_lstm_desc* d) {
   p.o_dh = o; o += al(2 * p.npix * HC * 4);
   p.o_dc = o; o += al(p.npix * HC * 4);
   p.o_dP = o; o += al(p.npix * GC * p.es * p.T);
-  p.o_dPsum = o; o += al(p.npix * GC * 4);
-  p.o_dPsumS = o; o += al(p.npix * GC * p.es);
+  // sum over steps of dP (static x: its bias / weight / input gradients need
+  // only that sum); per-step input: the bias sums come from dP itself
+  p.o_dPsum = o; o += p.xseq ? 0 : al(p.npix * GC * 4);
+  p.o_dPsumS = o; o += p.xseq ? 0 : al(p.npix * GC * p.es);
   p.o_jvP = o; o += al(2 * p.npix * GC * p.es);
   p.o_wsh = o; o += al((size_t)p.nsl_h * NG * KK * 1024 * 4);
   p.o_wsx = o; o += al((size_t)p.nsl_x * NG * KK * 1024 * 4);
   p.o_col = o; o += al((size_t)p.nb * GC * 4);
+  // per-step input: d x_t of all steps from ONE transposed conv over B*T images
+  p.o_dx = o; o += p.xseq ? al(p.npix * HC * 4 * p.T) : 0;
   p.ws = o;
   return p;
 }
@@ -955,10 +989,11 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   HIPCHK(hipGetLastError());
 
   S* xcl = (S*)(sv + p.o_x);
-  const size_t hstep0 = p.npix * HC;
-  for (int t = 0; t < (p.xseq ? p.T : 1); ++t)
-    hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, x, xcl + t * hstep0,
-                       p.B, p.cin, p.xseq ? p.T : 1, t);
+  if (p.xseq)
+    hipLaunchKernelGGL(k_to_cl_seq<S>, grid_for(p.npix * HC * p.T), dim3(256), 0, st, x, xcl,
+                       p.B, p.cin, p.T);
+  else
+    hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, x, xcl, p.B, p.cin);
   S* hinit = h0 ? (S*)(sv + p.o_h0) : nullptr;
   float* cinit = c0 ? (float*)(sv + p.o_c0) : nullptr;
   if (h0) hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, h0, hinit, p.B, p.ch);
@@ -971,15 +1006,15 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   const size_t pstep = p.npix * GC, hstep = p.npix * HC;
   // static x: xg = Wx*x + b once, P_t = xg + Wh*h_{t-1}; per-step x:
   // P_t = Wx*x_t + b, then += Wh*h_{t-1} in place
-  float* xg = h0 ? (float*)(sv + p.o_xg) : P;      // without h0, P_0 = xg
-  if (!p.xseq)
-    if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], xg, nullptr, pa.bias, p.B, st)) return rc;
+  // static x: xg = Wx*x + b (without h0, P_0 = xg); per-step x: the
+  // x-convolutions of all steps do not depend on h, so ONE launch over the
+  // B*T images writes every P_t = Wx*x_t + b ([T][B] image order in xcl and P)
+  float* xg = p.xseq ? nullptr : (h0 ? (float*)(sv + p.o_xg) : P);
+  if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], p.xseq ? P : xg, nullptr, pa.bias,
+                               p.xseq ? p.B * p.T : p.B, st))
+    return rc;
   for (int t = 0; t < p.T; ++t) {
     const S* hin = t == 0 ? hinit : H + (t - 1) * hstep;
-    if (p.xseq)
-      if (int rc = conv_k<S, 1, 4>(p.K, xcl + t * hstep, sv + p.o_fr[0], P + t * pstep, nullptr,
-                                   pa.bias, p.B, st))
-        return rc;
     if (hin)
       if (int rc = conv_k<S, 1, 4>(p.K, hin, sv + p.o_fr[1], P + t * pstep,
                                    p.xseq ? P + t * pstep : xg, nullptr, p.B, st))
@@ -1013,8 +1048,8 @@ int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
   float* dh = (float*)(ws + p.o_dh);
   float* dc = (float*)(ws + p.o_dc);
   S* dP = (S*)(ws + p.o_dP);
-  float* dPsum = (float*)(ws + p.o_dPsum);
-  S* dPsumS = (S*)(ws + p.o_dPsumS);
+  float* dPsum = p.xseq ? nullptr : (float*)(ws + p.o_dPsum);
+  S* dPsumS = p.xseq ? nullptr : (S*)(ws + p.o_dPsumS);
 
   hipLaunchKernelGGL(k_to_cl<float>, grid_for(p.npix * HC), dim3(256), 0, st, d_h, dh, p.B, p.ch);
   if (d_c)
@@ -1057,7 +1092,10 @@ int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
   wx.wslab = (float*)(ws + p.o_wsx);
   if (int rc = wgrad_k<S>(p.K, wx, st)) return rc;
   float* colp = (float*)(ws + p.o_col);
-  hipLaunchKernelGGL(k_lcolsum, dim3(p.nb), dim3(256), 0, st, (const float*)dPsum, colp, npix);
+  if (p.xseq)
+    hipLaunchKernelGGL(k_lcolsum<S>, dim3(p.nb), dim3(256), 0, st, (const S*)dP, colp, npix * p.T);
+  else
+    hipLaunchKernelGGL(k_lcolsum<float>, dim3(p.nb), dim3(256), 0, st, (const float*)dPsum, colp, npix);
   LReduceArgs ra{};
   ra.K = p.K; ra.nsl_h = p.nsl_h; ra.nsl_x = p.nsl_x; ra.ch = p.ch; ra.cin = p.cin; ra.nb = p.nb;
   ra.wslab_h = wa.wslab; ra.wslab_x = wx.wslab; ra.colpart = colp;
@@ -1065,12 +1103,17 @@ int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
   hipLaunchKernelGGL(k_lreduce, dim3(1024), dim3(256), 0, st, ra);
   HIPCHK(hipGetLastError());
   if (g->d_x) {
-    for (int t = 0; t < (p.xseq ? p.T : 1); ++t) {
-      if (int rc = conv_k<S, 4, 1>(p.K, p.xseq ? (const void*)(dP + t * pstep) : (const void*)dPsumS,
-                                   sv + p.o_fr[3], dh, nullptr, nullptr, p.B, st))
+    if (p.xseq) {        // all steps' d x_t from one transposed conv over the B*T images
+      float* dxs = (float*)(ws + p.o_dx);
+      if (int rc = conv_k<S, 4, 1>(p.K, dP, sv + p.o_fr[3], dxs, nullptr, nullptr, p.B * p.T, st))
+        return rc;
+      hipLaunchKernelGGL(k_from_cl_seq<float>, grid_for(p.npix * p.cin * p.T), dim3(256), 0, st,
+                         (const float*)dxs, g->d_x, p.B, p.cin, p.T);
+    } else {
+      if (int rc = conv_k<S, 4, 1>(p.K, dPsumS, sv + p.o_fr[3], dh, nullptr, nullptr, p.B, st))
         return rc;
       hipLaunchKernelGGL(k_from_cl<float>, grid_for(p.npix * p.cin), dim3(256), 0, st,
-                         (const float*)dh, g->d_x, p.B, p.cin, p.xseq ? p.T : 1, t);
+                         (const float*)dh, g->d_x, p.B, p.cin);
     }
     HIPCHK(hipGetLastError());
   }
@@ -1169,6 +1212,23 @@ int pt_lstm_jv_penalty(const pt_lstm_desc* d, const void* saved, void* workspace
   hipStream_t st = (hipStream_t)stream;
   return bf ? run_jv<bf16_t>(d, (const char*)saved, (char*)workspace, mu, jv, st)
             : run_jv<float>(d, (const char*)saved, (char*)workspace, mu, jv, st);
+}
+
+int pt_lstm_export_h(const pt_lstm_desc* d, const void* saved, float* h_seq,
+                     pt_lstm_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  if (!saved || !h_seq) return fail(PT_LSTM_ERR_ARG, "null saved / h_seq%ld");
+  const LPlan p = plan(d);
+  hipStream_t st = (hipStream_t)stream;
+  const char* H = (const char*)saved + p.o_h;
+  if (d->dtype == PT_LSTM_BF16)
+    hipLaunchKernelGGL(k_from_cl_seq<bf16_t>, grid_for(p.npix * p.ch * p.T), dim3(256), 0, st,
+                       (const bf16_t*)H, h_seq, p.B, p.ch, p.T);
+  else
+    hipLaunchKernelGGL(k_from_cl_seq<float>, grid_for(p.npix * p.ch * p.T), dim3(256), 0, st,
+                       (const float*)H, h_seq, p.B, p.ch, p.T);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 size_t pt_lstm_stem_workspace_bytes(int cin) {

@@ -156,6 +156,8 @@ class InT(nn.Module):
         self.kernel_size = kernel_size
         self.no_inh = no_inh
         self.cell_dtype = _DEFAULT_DTYPE
+        # ptamd.dist.CellDist: SyncBN / early-gradient all-reduce (None: per-replica BN)
+        self.cell_dist = None
 
     def cell_config(self):
         return CellConfig(ksize=self.kernel_size, act=_act_name(self.nl), no_inh=self.no_inh,
@@ -178,7 +180,8 @@ class InT(nn.Module):
 
     def forward(self, x, testmode=False):
         e_last, e_seq, gates = run_cell(x, self.cell_params(), self.cell_config(),
-                                        want_seq=testmode)
+                                        want_seq=testmode,
+                                        cdist=self.cell_dist)
         output = self.readout(e_last, x)
         if testmode:
             b, t, c, h, w = e_seq.shape

@@ -107,10 +107,12 @@ class ConvLSTMCell(nn.Module):
                 + [getattr(self, f"Wx{g}").bias for g in gs]
                 + [getattr(self, f"Wh{g}").weight for g in gs])
 
-    def steps(self, x, timesteps, h=None, c=None, want_jv=False, mu=0.9):
-        """``timesteps`` steps from (h, c) (None = zeros): (h_T, c_T, jv)."""
+    def steps(self, x, timesteps, h=None, c=None, want_jv=False, mu=0.9, want_seq=False):
+        """``timesteps`` steps from (h, c) (None = zeros): (h_T, c_T, jv), plus
+        every step's h [B,C,T,H,W] when ``want_seq``."""
         return run_steps(x, self.cell_weights(), ksize=self.kernel_size, steps=timesteps,
-                         h0=h, c0=c, dtype=self.cell_dtype, want_jv=want_jv, mu=mu)
+                         h0=h, c0=c, dtype=self.cell_dtype, want_jv=want_jv, mu=mu,
+                         want_seq=want_seq)
 
     def forward(self, x, h, c):
         h_t, c_t, _ = self.steps(x, 1, h, c)
@@ -213,7 +215,12 @@ class ConvLSTMVideo(nn.Module):
 
     ``forward(x, testmode=False)`` has InT's signature and returns
     ``(logits [B,1], jv_penalty)``, so engine.model_step / mainclean.py run it
-    (registry name ``convlstm``).
+    (registry name ``convlstm``).  ``testmode=True`` returns, as InT's
+    (InT.py:230-233,244), ``(logits, states [B,T,1,H,W], hidden [B,T,C,H,W])``:
+    ``states`` = readout_conv(h_t) per frame; the third element, InT's
+    attention maps there, is the per-frame hidden state h_t here (the
+    reference ConvLSTM's testmode collects exactly those, convlstm.py:127-135;
+    the cell has no attention gate).
     """
 
     def __init__(self, dimensions=25, timesteps=8, kernel_size=7, jacobian_penalty=False,
@@ -249,17 +256,21 @@ class ConvLSTMVideo(nn.Module):
     accepts_u8 = True
 
     def forward(self, x, testmode=False):
-        if testmode:
-            raise NotImplementedError("ConvLSTMVideo has no per-frame testmode outputs")
         # the 1x1x1 stem + softplus in one HBM pass (pt_lstm_stem_*); a
         # [C x 3] @ [3 x THW] library GEMM took 16 ms of a 88 ms step here
         xbn = lstm.stem(x, self.preproc.weight, self.preproc.bias)   # [B, C, T, H, W]
         steps = xbn.shape[2]
         want_jv = self.training and steps >= 2
-        h_t, _, jv = self.unit1.steps(xbn, steps, want_jv=want_jv)
+        res = self.unit1.steps(xbn, steps, want_jv=want_jv, want_seq=testmode)
+        h_t, jv = res[0], res[2]
         out = torch.cat([self.readout_conv(h_t), target_channel(x)[:, None]], 1)
         out = self.target_conv(out)
         out = F.avg_pool2d(out, kernel_size=out.size()[2:])
         out = self.readout_dense(out.reshape(x.shape[0], -1))
+        if testmode:
+            hidden = res[3].permute(0, 2, 1, 3, 4)                  # [B, T, C, H, W]
+            b, t, c, h, w = hidden.shape
+            states = self.readout_conv(hidden.reshape(b * t, c, h, w)).reshape(b, t, 1, h, w)
+            return out, states, hidden
         jv_penalty = jv if want_jv else torch.ones(1, device=x.device)
         return out, jv_penalty

@@ -127,6 +127,8 @@ class FFhGRU(nn.Module):
         self.nl = F.softplus
         self.kernel_size = kernel_size
         self.cell_dtype = _DEFAULT_DTYPE
+        # ptamd.dist.CellDist: SyncBN / early-gradient all-reduce (None: per-replica BN)
+        self.cell_dist = None
 
     def cell_config(self):
         return CellConfig(ksize=self.kernel_size, act="softplus", no_inh=False, cell="hgru",
@@ -149,7 +151,8 @@ class FFhGRU(nn.Module):
 
     def forward(self, x, testmode=False):
         e_last, e_seq, gates = run_cell(x, self.cell_params(), self.cell_config(),
-                                        want_seq=testmode)
+                                        want_seq=testmode,
+                                        cdist=self.cell_dist)
         output = self.readout(e_last, x)
         if testmode:
             b, t, c, h, w = e_seq.shape

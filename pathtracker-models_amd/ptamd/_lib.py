@@ -20,7 +20,8 @@ PT_X_F32_NCTHW, PT_X_U8_NTHWC = 0, 1
 
 # Exported symbols declared in include/pt_cell.h (tests check all are present).
 EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
-           "pt_cell_export_exc", "pt_cell_backward", "pt_cell_timing_enable",
+           "pt_cell_export_exc", "pt_cell_backward", "pt_cell_bn_sync_doubles",
+           "pt_cell_forward_dist", "pt_cell_backward_dist", "pt_cell_timing_enable",
            "pt_cell_timing_read", "pt_cell_timing_reset", "pt_last_error", "pt_version")
 
 # kernel kinds for pt_cell_timing_* (include/pt_cell.h)
@@ -48,6 +49,16 @@ class Params(ctypes.Structure):
 
 class Grads(ctypes.Structure):
     _fields_ = Params._fields_
+
+
+# int (*)(void* user, int64_t offset, int64_t count): SyncBN all-reduce hook
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64)
+
+
+class Dist(ctypes.Structure):
+    """pt_cell_dist (include/pt_cell.h): SyncBN hook and the early-gradient event."""
+    _fields_ = [("bn_world", ctypes.c_int32), ("bn_buf", _P), ("allreduce", ALLREDUCE_FN),
+                ("user", _P), ("grads_early_event", _P)]
 
 
 class PtCellError(RuntimeError):
@@ -81,6 +92,15 @@ def load():
         lib.pt_cell_backward.restype = ctypes.c_int
         lib.pt_cell_backward.argtypes = [ctypes.POINTER(Desc), _P, ctypes.POINTER(Params), _P, _P,
                                          _P, ctypes.POINTER(Grads), _P]
+        lib.pt_cell_bn_sync_doubles.restype = ctypes.c_size_t
+        lib.pt_cell_bn_sync_doubles.argtypes = [ctypes.POINTER(Desc)]
+        lib.pt_cell_forward_dist.restype = ctypes.c_int
+        lib.pt_cell_forward_dist.argtypes = [ctypes.POINTER(Desc), _P, ctypes.POINTER(Params), _P,
+                                             _P, _P, _P, ctypes.POINTER(Dist), _P]
+        lib.pt_cell_backward_dist.restype = ctypes.c_int
+        lib.pt_cell_backward_dist.argtypes = [ctypes.POINTER(Desc), _P, ctypes.POINTER(Params), _P,
+                                              _P, _P, ctypes.POINTER(Grads), ctypes.POINTER(Dist),
+                                              _P]
         lib.pt_cell_timing_enable.restype = ctypes.c_int
         lib.pt_cell_timing_enable.argtypes = [ctypes.c_uint32]
         lib.pt_cell_timing_read.restype = ctypes.c_int

@@ -10,10 +10,10 @@ BPTT through it (mainclean.py:204).
 from __future__ import annotations
 
 import ctypes
-import weakref
 from dataclasses import dataclass
 
 import torch
+from torch.utils.weak import WeakTensorKeyDictionary
 
 from . import _lib
 
@@ -84,8 +84,10 @@ def _desc(cfg: CellConfig, x: torch.Tensor, channels: int) -> _lib.Desc:
 # to another dtype): one persistent buffer per parameter, refreshed in place
 # each call, so the device pointers -- and with them the library's cached
 # hipGraph (pt_graph.h, keyed by every pointer) -- stay the same from step to
-# step instead of a fresh temporary forcing a re-capture per call.
-_STAGED = weakref.WeakKeyDictionary()
+# step instead of a fresh temporary forcing a re-capture per call.  Keys
+# compare by identity (a plain WeakKeyDictionary would compare tensors
+# element-wise on a hash collision and raise).
+_STAGED = WeakTensorKeyDictionary()
 
 
 def _as_f32(p):
@@ -133,14 +135,17 @@ class RecurrentCellFn(torch.autograd.Function):
     (converted inside the kernels, bit-identical to engine.prepare_data).
 
     E_seq / att are only filled when ``want_seq`` (testmode); otherwise they
-    are empty tensors.  Only E_T is differentiable.
+    are empty tensors.  Only E_T is differentiable.  ``cdist`` (a
+    ptamd.dist.CellDist or None) selects SyncBN and the early-gradient
+    all-reduce (pt_cell_dist).
     """
 
     @staticmethod
-    def forward(ctx, x, cfg: CellConfig, want_seq: bool, *params):
+    def forward(ctx, x, cfg: CellConfig, want_seq: bool, cdist, *params):
         _require_device(x)
         lib = _lib.load()
         x = x.contiguous() if x.dtype == torch.uint8 else x.contiguous().float()
+        ctx.param_ids = [id(p) if p is not None else None for p in params]
         params = [_as_f32(p) for p in params]
         c = params[0].shape[0]
         d = _desc(cfg, x, c)
@@ -156,14 +161,18 @@ class RecurrentCellFn(torch.autograd.Function):
                             device=x.device)
         pp = _pack(_lib.Params, params)
         st = _stream(x.device)
-        _lib.check(lib.pt_cell_forward(ctypes.byref(d), _ptr(x), ctypes.byref(pp), _ptr(saved),
-                                       _ptr(ws), _ptr(e_last), _ptr(gates) if want_seq else None,
-                                       st))
+        dd = (cdist.struct(lib.pt_cell_bn_sync_doubles(ctypes.byref(d)), x.device)
+              if cdist is not None else None)
+        _lib.check(lib.pt_cell_forward_dist(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
+                                            _ptr(saved), _ptr(ws), _ptr(e_last),
+                                            _ptr(gates) if want_seq else None,
+                                            ctypes.byref(dd) if dd is not None else None, st))
         e_seq = torch.empty((b, t, c, h, w) if want_seq else (0,), dtype=torch.float32,
                             device=x.device)
         if want_seq:
             _lib.check(lib.pt_cell_export_exc(ctypes.byref(d), _ptr(saved), _ptr(e_seq), st))
         ctx.cfg = cfg
+        ctx.cdist = cdist
         ctx.saved_blob = saved
         ctx.save_for_backward(x, *[p if p is not None else torch.empty(0) for p in params])
         ctx.has = [p is not None for p in params]
@@ -190,13 +199,31 @@ class RecurrentCellFn(torch.autograd.Function):
                  for i, p in enumerate(params)]
         pp = _pack(_lib.Params, params)
         gg = _pack(_lib.Grads, grads)
-        _lib.check(lib.pt_cell_backward(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
-                                        _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_e_last),
-                                        ctypes.byref(gg), _stream(x.device)))
+        cdist = ctx.cdist
+        early = None
+        bucket = cdist.bucket if cdist is not None else None
+        if bucket is not None and cdist.world() > 1:
+            early = torch.cuda.Event()
+            early.record()                  # creates the event; the library re-records it
+        dd = (cdist.struct(lib.pt_cell_bn_sync_doubles(ctypes.byref(d)), x.device,
+                           early.cuda_event if early is not None else None)
+              if cdist is not None else None)
+        _lib.check(lib.pt_cell_backward_dist(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
+                                             _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_e_last),
+                                             ctypes.byref(gg),
+                                             ctypes.byref(dd) if dd is not None else None,
+                                             _stream(x.device)))
+        if early is not None:
+            # every gradient but the two k x k weights is final at `early`:
+            # averaged on a side stream under the k x k weight-gradient kernel
+            from .dist import LATE_KEYS
+            bucket.reduce_early([(pid, g) for k, pid, g in zip(PARAM_KEYS, ctx.param_ids, grads)
+                                 if g is not None and k not in LATE_KEYS], early)
         ctx.saved_blob = None
-        return (None, None, None, *grads)
+        return (None, None, None, None, *grads)
 
 
-def run_cell(x, params, cfg: CellConfig, want_seq: bool = False):
-    """Apply the HIP recurrent cell.  ``params`` is a list in PARAM_KEYS order."""
-    return RecurrentCellFn.apply(x, cfg, want_seq, *params)
+def run_cell(x, params, cfg: CellConfig, want_seq: bool = False, cdist=None):
+    """Apply the HIP recurrent cell.  ``params`` is a list in PARAM_KEYS order;
+    ``cdist``: optional ptamd.dist.CellDist (SyncBN / early-gradient overlap)."""
+    return RecurrentCellFn.apply(x, cfg, want_seq, cdist, *params)

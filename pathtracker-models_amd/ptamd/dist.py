@@ -2,19 +2,34 @@
 
 The reference scales with single-process ``nn.DataParallel`` (mainclean.py:132-134):
 parameters broadcast, input scattered from cuda:0, gradients reduce-added.
-Here every rank owns its clips (no scatter), computes its own BatchNorm batch
-statistics (exactly DataParallel's per-replica semantics), and the only
-exchange is ONE all-reduce per step of a single flat fp32 gradient bucket
-(107,190 parameters = 428,760 B for InT), over RCCL/xGMI (backend "nccl") on
-GPUs or gloo on CPU.  The bucket is far below any per-link bandwidth concern;
-the all-reduce is latency-bound (tens of microseconds).
+Here every rank owns its clips (no scatter) and the only exchange of the
+default mode is ONE averaging of the fp32 gradients per step (107,190
+parameters = 428,760 B for InT) over RCCL/xGMI (backend "nccl") on GPUs or gloo
+on CPU.  BatchNorm statistics are per replica by default -- exactly
+DataParallel's semantics.
+
+Two opt-in extensions of the HIP cell's C-ABI (``pt_cell_dist``,
+include/pt_cell.h), configured through :class:`CellDist`:
+
+* SyncBN: every BatchNorm reduction of the cell (2 per frame forward, 2 per
+  frame backward) is summed over the ranks before it is used, so the ranks
+  together compute exactly the single-process batch (4 T small all-reduces per
+  step, host callbacks between launches, no hipGraph replay);
+* gradient overlap: the cell's gradients other than the two k x k weights are
+  final before the k x k weight-gradient kernel (~2.5 ms at the headline
+  size) starts; :class:`GradBucket` averages them on a side stream while that
+  kernel runs, and only the k x k weights (and the readout) afterwards.
 """
 from __future__ import annotations
 
 import os
+import traceback
 
 import torch
 import torch.distributed as dist
+
+# cell gradients final before the k x k weight-gradient kernel (ptamd.cell.PARAM_KEYS)
+LATE_KEYS = ("unit1.w_exc", "unit1.w_inh")
 
 
 def env_rank():
@@ -22,34 +37,128 @@ def env_rank():
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
-class GradBucket:
-    """Flat fp32 gradient bucket averaged across ranks with one all-reduce."""
+def _world(group=None):
+    return dist.get_world_size(group) if dist.is_initialized() else 1
 
-    def __init__(self, params, device):
+
+class GradBucket:
+    """fp32 gradients averaged across ranks with one all-reduce of a flat bucket
+    (plus, with a :class:`CellDist` overlap, one earlier side-stream all-reduce
+    of the cell's early gradients)."""
+
+    def __init__(self, params, device, group=None):
         self.params = [p for p in params if p.requires_grad]
         self.numel = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.group = group
+        self._early_done = set()        # ids of params averaged early this step
+        self._side = None
 
-    def allreduce_mean(self, group=None):
-        world = dist.get_world_size(group) if dist.is_initialized() else 1
+    def reduce_early(self, pairs, event):
+        """Average the (id(param), grad) pairs on a side stream that waits for
+        ``event`` (recorded by the cell's backward once those gradients are
+        written), and make the current stream wait for it -- the wait is
+        enqueued behind the k x k weight-gradient kernel, which the all-reduce
+        therefore overlaps.  Called from the cell's autograd backward."""
+        world = _world(self.group)
+        if world == 1 or not pairs:
+            return
+        main = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=main.device)
+        side = self._side
+        side.wait_event(event)
+        with torch.cuda.stream(side):
+            flat = torch.cat([g.reshape(-1) for _, g in pairs])
+            dist.all_reduce(flat, group=self.group)
+            flat.mul_(1.0 / world)
+            off = 0
+            for _, g in pairs:
+                n = g.numel()
+                g.copy_(flat[off:off + n].view_as(g))
+                g.record_stream(side)
+                off += n
+        main.wait_stream(side)
+        self._early_done = {pid for pid, _ in pairs}
+
+    def allreduce_mean(self):
+        world = _world(self.group)
         if world == 1:
             return
+        pend = [p for p in self.params if id(p) not in self._early_done]
+        self._early_done = set()
+        n_all = sum(p.numel() for p in pend)
+        flat = self.flat[:n_all]
         off = 0
-        for p in self.params:
+        for p in pend:
             n = p.numel()
             if p.grad is None:
-                self.flat[off:off + n].zero_()
+                flat[off:off + n].zero_()
             else:
-                self.flat[off:off + n].copy_(p.grad.reshape(-1))
+                flat[off:off + n].copy_(p.grad.reshape(-1))
             off += n
-        dist.all_reduce(self.flat, group=group)
-        self.flat.mul_(1.0 / world)
+        dist.all_reduce(flat, group=self.group)
+        flat.mul_(1.0 / world)
         off = 0
-        for p in self.params:
+        for p in pend:
             n = p.numel()
             if p.grad is not None:          # params no rank differentiates stay None
-                p.grad.copy_(self.flat[off:off + n].view_as(p))
+                p.grad.copy_(flat[off:off + n].view_as(p))
             off += n
+
+
+class CellDist:
+    """Cross-replica options of the HIP cell (``pt_cell_dist``).
+
+    sync_bn: BatchNorm statistics over every rank's clips.  The library writes
+      each reduction's per-rank totals into ``bn_buf`` (fp64, on the device) and
+      calls back :meth:`allreduce_slice`, which SUMs that slice over ``group``
+      on the current stream.
+    bucket: a :class:`GradBucket` to average the early cell gradients on a side
+      stream while the k x k weight-gradient kernel runs (GPU ranks).
+    """
+
+    def __init__(self, group=None, sync_bn=False, bucket=None):
+        from . import _lib
+        self.group = group
+        self.sync_bn = sync_bn
+        self.bucket = bucket
+        self.bn_buf = None
+        self.failed = None
+        self._cfn = _lib.ALLREDUCE_FN(self._callback)    # kept alive with self
+
+    def world(self):
+        return _world(self.group)
+
+    def buffer(self, n, device):
+        if self.bn_buf is None or self.bn_buf.numel() < n or self.bn_buf.device != device:
+            self.bn_buf = torch.zeros(n, dtype=torch.float64, device=device)
+        return self.bn_buf
+
+    def allreduce_slice(self, offset, count):
+        dist.all_reduce(self.bn_buf[offset:offset + count], group=self.group)
+
+    def _callback(self, _user, offset, count):
+        try:
+            self.allreduce_slice(int(offset), int(count))
+            return 0
+        except Exception as e:      # the library turns a non-zero return into an error
+            self.failed = e
+            traceback.print_exc()
+            return 1
+
+    def struct(self, bn_doubles, device, early_event=None):
+        """The pt_cell_dist for one call (``bn_doubles`` = pt_cell_bn_sync_doubles)."""
+        from . import _lib
+        d = _lib.Dist()
+        world = self.world()
+        d.bn_world = world if self.sync_bn else 1
+        if d.bn_world > 1:
+            d.bn_buf = self.buffer(bn_doubles, device).data_ptr()
+            d.allreduce = self._cfn
+        d.user = None
+        d.grads_early_event = early_event
+        return d
 
 
 def lockstep(iterable, device):

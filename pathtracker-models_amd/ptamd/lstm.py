@@ -27,7 +27,8 @@ PT_LSTM_OK, PT_LSTM_ERR_ARG, PT_LSTM_ERR_UNSUPPORTED, PT_LSTM_ERR_HIP = 0, 1, 2,
 
 # Exported symbols declared in include/pt_lstm.h (tests check all are present).
 EXPORTS = ("pt_lstm_saved_bytes", "pt_lstm_workspace_bytes", "pt_lstm_forward",
-           "pt_lstm_backward", "pt_lstm_jv_penalty", "pt_lstm_stem_workspace_bytes",
+           "pt_lstm_backward", "pt_lstm_jv_penalty", "pt_lstm_export_h",
+           "pt_lstm_stem_workspace_bytes",
            "pt_lstm_stem_forward", "pt_lstm_stem_backward", "pt_lstm_last_error",
            "pt_lstm_version")
 
@@ -81,6 +82,8 @@ def load():
         lib.pt_lstm_backward.argtypes = [D, _P, _P, _P, _P, ctypes.POINTER(Grads), _P]
         lib.pt_lstm_jv_penalty.restype = ctypes.c_int
         lib.pt_lstm_jv_penalty.argtypes = [D, _P, _P, ctypes.c_float, _P, _P]
+        lib.pt_lstm_export_h.restype = ctypes.c_int
+        lib.pt_lstm_export_h.argtypes = [D, _P, _P, _P]
         lib.pt_lstm_stem_workspace_bytes.restype = ctypes.c_size_t
         lib.pt_lstm_stem_workspace_bytes.argtypes = [ctypes.c_int]
         _i, _ll = ctypes.c_int, ctypes.c_longlong
@@ -137,17 +140,18 @@ GATES = ("i", "f", "c", "o")
 
 
 class LSTMStepsFn(torch.autograd.Function):
-    """(x, h0|None, c0|None, 12 weights) -> (h_T, c_T, jv).
+    """(x, h0|None, c0|None, 12 weights) -> (h_T, c_T, jv, h_seq).
 
     ``jv`` (the training-mode Jacobian penalty, models/convlstm.py:150-161) is
     only computed when ``want_jv``; it is returned detached (the reference
     builds a graph for it only with ``jacobian_penalty=True``, and never puts
-    it in the loss it returns).
+    it in the loss it returns).  ``h_seq`` [B,ch,T,H,W] holds every step's
+    hidden state when ``want_seq`` (testmode), detached; otherwise it is empty.
     """
 
     @staticmethod
     def forward(ctx, x, h0, c0, ksize: int, steps: int, dtype: str, want_jv: bool, mu: float,
-                *weights):
+                want_seq: bool, *weights):
         _require_device(x)
         lib = load()
         x = x.contiguous().float()
@@ -178,16 +182,19 @@ class LSTMStepsFn(torch.autograd.Function):
             jv = torch.empty_like(h_out)
             check(lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
                                          _ptr(jv), st))
+        h_seq = torch.empty((b, ch, steps, hh, ww) if want_seq else (0,), device=x.device)
+        if want_seq:
+            check(lib.pt_lstm_export_h(ctypes.byref(d), _ptr(saved), _ptr(h_seq), st))
         ctx.meta = (ksize, steps, dtype, h0 is not None, c0 is not None, tuple(x.shape), ch)
         ctx.desc = d
         ctx.saved_blob = saved
         ctx.wshapes = [w.shape for w in weights]
-        ctx.mark_non_differentiable(jv)
-        return h_out, c_out, jv
+        ctx.mark_non_differentiable(jv, h_seq)
+        return h_out, c_out, jv, h_seq
 
     @staticmethod
     @once_differentiable
-    def backward(ctx, d_h, d_c, _d_jv):
+    def backward(ctx, d_h, d_c, _d_jv, _d_seq):
         # may run several times on one graph (retain_graph: the rbp Neumann
         # series and the Jacobian-penalty VJPs, models/convlstm.py:35,155-160),
         # so the saved blob stays with ctx until autograd frees the graph
@@ -218,13 +225,16 @@ class LSTMStepsFn(torch.autograd.Function):
         gg.d_c0 = dc0.data_ptr() if dc0 is not None else 0
         check(lib.pt_lstm_backward(ctypes.byref(d), _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_h),
                                    _ptr(d_c), ctypes.byref(gg), _stream(dev)))
-        return (dx, dh0, dc0, None, None, None, None, None, *grads)
+        return (dx, dh0, dc0, None, None, None, None, None, None, *grads)
 
 
 def run_steps(x, weights, *, ksize: int, steps: int, h0=None, c0=None, dtype: str = "f32",
-              want_jv: bool = False, mu: float = 0.9):
-    """Apply ``steps`` ConvLSTM steps.  ``weights``: [Wx_i..o, bx_i..o, Wh_i..o]."""
-    return LSTMStepsFn.apply(x, h0, c0, ksize, steps, dtype, want_jv, mu, *weights)
+              want_jv: bool = False, mu: float = 0.9, want_seq: bool = False):
+    """Apply ``steps`` ConvLSTM steps.  ``weights``: [Wx_i..o, bx_i..o, Wh_i..o].
+    Returns (h_T, c_T, jv, h_seq) when ``want_seq``, else (h_T, c_T, jv)."""
+    h, c, jv, seq = LSTMStepsFn.apply(x, h0, c0, ksize, steps, dtype, want_jv, mu, want_seq,
+                                      *weights)
+    return (h, c, jv, seq) if want_seq else (h, c, jv)
 
 
 class StemFn(torch.autograd.Function):

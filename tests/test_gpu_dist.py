@@ -1,0 +1,138 @@
+"""Multi-rank paths of the HIP cell on ONE GPU (2 processes, gloo on device
+tensors): the cross-replica hooks of include/pt_cell.h (pt_cell_dist) through
+ptamd.dist.CellDist, against the single-process HIP cell.
+
+* SyncBN: 2 ranks x 2 clips with BatchNorm statistics all-reduced between
+  the cell's launches reproduce the single process on all 4 clips (logits per
+  clip, rank-averaged gradients) -- the library's per-reduction callback, the
+  SyncBN totals kernel and the global clip count in every consumer.
+* early-gradient overlap: with per-replica BatchNorm (the default) the
+  gradients averaged in two parts -- the cell's early gradients on a side
+  stream behind the event the backward records before its k x k
+  weight-gradient kernel, the rest after backward -- equal the mean of the
+  per-shard single-process gradients.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    from models import InT
+    torch.manual_seed(21)
+    m = InT.InT(dimensions=32, timesteps=6, kernel_size=7)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
+                p.uniform_(0.5, 1.5)
+            elif n.endswith(("mu", "gamma")):
+                p.uniform_(-0.5, 0.5)
+    return m
+
+
+def _batch():
+    from ptamd import synth
+    clips, labels = synth.make_batch(5, 4, 6)
+    x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float()
+    return x, torch.tensor([ord(v) for v in labels], dtype=torch.float32)
+
+
+def _worker(rank, world, port, sync_bn, out_q):
+    import sys
+    sys.path[:0] = [os.path.join(REPO, "tests"), REPO, os.path.join(REPO, "pathtracker-models_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from ptamd.dist import CellDist, GradBucket
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _model().to(dev)
+    x, y = _batch()
+    sh = slice(2 * rank, 2 * rank + 2)
+    bucket = GradBucket(m.parameters(), dev)
+    m.cell_dist = CellDist(sync_bn=sync_bn, bucket=bucket)
+    out, _ = m(x[sh].to(dev))
+    F.binary_cross_entropy_with_logits(out, y[sh].to(dev).reshape(-1, 1)).backward()
+    early = len(bucket._early_done)
+    bucket.allreduce_mean()
+    torch.cuda.synchronize()
+    out_q.put((rank, out.detach().cpu().numpy(), early,
+               {k: p.grad.detach().cpu().numpy() for k, p in m.named_parameters()
+                if p.grad is not None}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_ranks(sync_bn):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sync_bn, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=200) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _single(x, y):
+    dev = torch.device("cuda:0")
+    m = _model().to(dev)
+    out, _ = m(x.to(dev))
+    F.binary_cross_entropy_with_logits(out, y.to(dev).reshape(-1, 1)).backward()
+    return out.detach().cpu(), {k: p.grad.detach().cpu() for k, p in m.named_parameters()
+                                if p.grad is not None}
+
+
+def _close_grads(got, ref, rel):
+    assert set(got) == set(ref)
+    for k, v in got.items():
+        err = float((torch.from_numpy(v) - ref[k]).abs().max())
+        assert err <= 1e-7 + rel * float(ref[k].abs().max()), (k, err)
+
+
+@pytest.mark.timeout(300)
+def test_syncbn_two_ranks_equal_single_process():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    res = _run_ranks(sync_bn=True)
+    x, y = _batch()
+    lo, g = _single(x, y)
+    for r in (0, 1):
+        logits, early, grads = res[r]
+        torch.testing.assert_close(torch.from_numpy(logits), lo[2 * r:2 * r + 2], rtol=0, atol=1e-5)
+        assert early > 0                                 # the side-stream part ran
+        _close_grads(grads, g, 1e-5)
+
+
+@pytest.mark.timeout(300)
+def test_early_gradient_overlap_matches_shard_mean():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    res = _run_ranks(sync_bn=False)
+    x, y = _batch()
+    parts = [_single(x[s], y[s]) for s in (slice(0, 2), slice(2, 4))]
+    mean = {k: (parts[0][1][k] + parts[1][1][k]) / 2 for k in parts[0][1]}
+    for r in (0, 1):
+        logits, early, grads = res[r]
+        torch.testing.assert_close(torch.from_numpy(logits), parts[r][0], rtol=0, atol=1e-6)
+        assert early == 22                               # every cell param but w_exc / w_inh
+        _close_grads(grads, mean, 1e-5)

@@ -3,12 +3,13 @@
 * smallest shapes against the CPU oracle (f32, 1e-3): one clip, one frame;
   an odd batch with two frames; a single-clip 64x64 hGRU (tiles, B=1);
 * raw u8 clips [B,T,H,W,3] as the cell input (PT_X_U8_NTHWC) against the
-  f32 tensor engine.prepare_data builds from them: same values, so logits and
-  gradients agree to fp64-atomic summation order (InT f32 / bf16, tiled hGRU);
+  f32 tensor engine.prepare_data builds from them: same values, so the cell's
+  outputs and gradients agree bit for bit (InT f32 / bf16, tiled hGRU);
 * at the headline size (B=256, T=64, bf16) where the oracle is too slow:
   permutation equivariance (BatchNorm's batch statistics are symmetric in the
-  clips, so permuting the clips permutes the logits; fp64 statistics sums make
-  the result order-independent to rounding) and run-to-run reproducibility.
+  clips, so permuting the clips permutes the logits, up to the rounding of the
+  fp64 statistics sums taken in the permuted order) and bitwise run-to-run
+  reproducibility.
 """
 
 import numpy as np
@@ -103,10 +104,13 @@ def test_u8_input_matches_f32_input(cell, dtype, hw):
                                            for k, p in m.named_parameters() if p.grad is not None}))
     (o0, g0), (o1, g1) = res
     assert torch.isfinite(o1).all()
-    _close("logits", o1, o0, 1e-6)
+    assert torch.equal(o1, o0)
     assert g0.keys() == g1.keys()
     for k in g0:
-        _close(f"grad {k}", g1[k], g0[k], 1e-7, 1e-5)
+        if k.startswith(("unit1.", "preproc.")):      # the library's own gradients
+            assert torch.equal(g1[k], g0[k]), k
+        else:                                          # readout: MIOpen / hipBLASLt
+            _close(f"grad {k}", g1[k], g0[k], 1e-7, 1e-5)
 
 
 def _headline_model(dev):
@@ -129,10 +133,16 @@ def test_headline_size_permutation_and_reproducibility():
     m.zero_grad(set_to_none=True)
     out2, _ = m(x)                                       # same input again
     F.binary_cross_entropy_with_logits(out2, y.reshape(-1, 1)).backward()
-    _close("rerun logits", out2, out1, 1e-6)
+    # the cell is bitwise reproducible (deterministic BatchNorm sums); the
+    # readout's MIOpen/hipBLASLt gradients need not be, so only the cell's
+    # parameters (the library's own output) are compared bit for bit
+    assert torch.equal(out2, out1)
     for k, p in m.named_parameters():
         if p.grad is not None:
-            _close(f"rerun grad {k}", p.grad, g1[k], 1e-7, 1e-5)
+            if k.startswith(("unit1.", "preproc.")):
+                assert torch.equal(p.grad, g1[k]), k
+            else:
+                _close(f"rerun grad {k}", p.grad, g1[k], 1e-7, 1e-5)
     m.zero_grad(set_to_none=True)
     out3, _ = m(x[perm].contiguous())                    # clips permuted
     F.binary_cross_entropy_with_logits(out3, y[perm].reshape(-1, 1)).backward()

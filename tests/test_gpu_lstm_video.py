@@ -181,3 +181,38 @@ def test_bf16_matches_f32_at_cfg3_size():
     assert flips == {"train_0.5": 0, "eval_0": 0}, rec
     bad = {n: v for n, v in cos.items() if v < 0.99}
     assert not bad, (bad, rec)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_testmode_per_frame_outputs(dtype):
+    """testmode returns InT's triple (InT.py:230-233,244): logits, per-frame
+    states = readout_conv(h_t) [B,T,1,H,W] and the per-frame hidden states
+    h_t [B,T,C,H,W] (what the reference ConvLSTM's testmode collects,
+    convlstm.py:127-135), each frame against the oracle's trajectory (f32:
+    1e-3; bf16: the stated bf16 tolerance, 2e-2 absolute on states/logits)."""
+    from oracle import cells
+    dev = _dev()
+    m = _model(7, 21)
+    x, _ = _clips(22, 3, 6)
+    sd = {n: p.detach().clone() for n, p in m.named_parameters()}
+    with torch.no_grad():
+        lo, _, hs, _ = cells.convlstm_video_forward(sd, x)
+        ref_h = torch.stack(hs, 1)                                   # [B,T,C,H,W]
+        ref_states = torch.stack([F.conv2d(h, sd["readout_conv.weight"], sd["readout_conv.bias"])
+                                  for h in hs], 1)
+    m = m.to(dev).eval()
+    m.cell_dtype = dtype
+    with torch.no_grad():
+        out, states, hidden = m(x.to(dev), testmode=True)
+        out2, _ = m(x.to(dev))
+    assert states.shape == (3, 6, 1, 32, 32) and hidden.shape == (3, 6, 25, 32, 32)
+    tol = 1e-3 if dtype == "f32" else 2e-2
+    assert float((out.cpu() - lo).abs().max()) < tol
+    assert torch.equal(out, out2)                       # testmode does not change the logits
+    for t in range(6):
+        assert float((hidden[:, t].cpu() - ref_h[:, t]).abs().max()) < tol, t
+        assert float((states[:, t].cpu() - ref_states[:, t]).abs().max()) < tol, t
+    # engine.model_step(test=True) path (utils/engine.py:64-72)
+    from utils import engine
+    res = engine.model_step(m, x.to(dev), "convlstm", test=True)
+    assert len(res) == 3 and torch.equal(res[0], out)

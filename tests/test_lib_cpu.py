@@ -216,3 +216,20 @@ def test_convlstm_no_cpu_fallback():
     with pytest.raises(RuntimeError, match="ROCm device"):
         m(torch.rand(1, 1, 32, 32), 0, 0, torch.zeros(1, 32, 32, dtype=torch.long),
           torch.nn.CrossEntropyLoss())
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.bfloat16])
+def test_param_staging_cache_reuses_its_buffer(dtype):
+    """Non-f32 parameters are staged into ONE persistent f32 buffer per
+    parameter (stable device pointers for the cached hipGraph): a second
+    lookup must return the same buffer, refreshed, not raise (a tensor-keyed
+    WeakKeyDictionary compares keys element-wise)."""
+    from ptamd.cell import _as_f32
+    p = torch.nn.Parameter(torch.randn(5, 3, dtype=dtype))
+    a = _as_f32(p)
+    b = _as_f32(p)
+    assert a is b and a.dtype == torch.float32
+    with torch.no_grad():
+        p.add_(1)
+    c = _as_f32(p)
+    assert c is a and torch.equal(c, p.detach().float())
