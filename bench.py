@@ -14,8 +14,10 @@ from the environment (WORLD_SIZE must equal N); run directly, bench.py starts
 torch.distributed.run itself as a child process before touching the GPU.  Rank
 0 prints ONE JSON line.  value = clips/s of the whole job (all ranks) =
 N * B * K / max-over-ranks(time of K steps).  Scaling is weak (B fixed per GPU).
-allreduce_ms_per_step: device time of the gradient all-reduce (exposed: the
-cell's weight gradients are all final only when the BPTT sweep reaches t=0).
+allreduce_ms_per_step: device time of the gradient all-reduce left after
+backward (the exposed part: by default the cell's early gradients -- all but
+the two k x k weights -- are averaged on a side stream under the k x k
+weight-gradient kernel; --no-grad-overlap averages everything here).
 
 roofline: the dominant kernel (largest summed device time over K further,
 instrumented steps, measured with HIP events the library records around its
@@ -63,14 +65,20 @@ def gate_flops():          # one 1x1 C->C gate conv over one clip frame
     return 2 * C * C * HW * HW
 
 
-def algorithmic_flops(kind, batch, frames):
+def algorithmic_flops(kind, batch, frames, fused=False):
     """Algorithmic FLOPs of ALL launches of one kernel kind in one step.
 
     Counts the model's contractions only (no recompute): forward conv + gates;
     backward data-gradients + 1x1 weight-gradients; the k x k weight gradients
     in k_wgrad.  Sum over kinds = 3 x forward (41.9 GFLOP/clip
-    at T=64, minus the stem's 12.6 MFLOP which is counted nowhere)."""
+    at T=64, minus the stem's 12.6 MFLOP which is counted nowhere).  fused: the
+    forward runs as k_fused_fa / k_fused_fb (point-wise + conv per launch) and
+    one k_pw_fa that only closes the last frame."""
     cf, gf = conv_flops(), gate_flops()
+    if fused:
+        fwd = {"k_fused_fa": frames * (cf + 4 * gf), "k_fused_fb": frames * (cf + 2 * gf)}
+        if kind in fwd or kind in ("k_pw_fa", "k_pw_fb", "k_conv_fa", "k_conv_fb"):
+            return fwd.get(kind, 0) * batch
     per_clip = {
         "k_conv_fa": frames * cf,                   # conv(gE, w_inh)
         "k_conv_fb": frames * cf,                   # conv(I, w_exc)
@@ -85,7 +93,7 @@ def algorithmic_flops(kind, batch, frames):
     return per_clip.get(kind, 0) * batch
 
 
-def algorithmic_bytes(kind, batch, frames, elt, xb=4):
+def algorithmic_bytes(kind, batch, frames, elt, xb=4, fused=False):
     """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
     (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
     XF = one clip-frame of the input (3x32x32; xb = 4 B f32, 1 B raw u8 clips).
@@ -95,6 +103,12 @@ def algorithmic_bytes(kind, batch, frames, elt, xb=4):
     sums) is not algorithmic and is not counted."""
     F, XF = C * HW * HW * elt, 3 * HW * HW * xb
     dE = C * HW * HW * (4 - elt)
+    if fused:       # the conv reads its input from the LDS tile the point-wise half wrote
+        fwd = {"k_fused_fa": frames * (XF + 7 * F + 2 * dE + F),
+               "k_fused_fb": frames * (XF + 3 * F + F),
+               "k_pw_fa": 3 * F + 2 * (F + dE)}          # closes E_{T-1} only
+        if kind in fwd or kind in ("k_pw_fb", "k_conv_fa", "k_conv_fb"):
+            return fwd.get(kind, 0) * batch
     per_clip = {
         "k_pw_fa": frames * (XF + 7 * F + 2 * dE),
         "k_conv_fa": frames * 2 * F,
@@ -208,12 +222,12 @@ def cpu_baseline(seconds, frames=64, batch=4):
                       f"{n} steps in {el:.1f}s"}
 
 
-def kernel_roofline(kind, ms, n, batch, frames, steps, dtype, xb):
+def kernel_roofline(kind, ms, n, batch, frames, steps, dtype, xb, fused=False):
     """One kernel kind against whichever roofline binds it (the larger ideal
     time: algorithmic FLOP / dense MFMA peak vs algorithmic bytes / HBM peak)."""
     elt = 2 if dtype == "bf16" else 4
-    fl = algorithmic_flops(kind, batch, frames) * steps / max(n, 1)
-    by = algorithmic_bytes(kind, batch, frames, elt, xb) * steps / max(n, 1)
+    fl = algorithmic_flops(kind, batch, frames, fused) * steps / max(n, 1)
+    by = algorithmic_bytes(kind, batch, frames, elt, xb, fused) * steps / max(n, 1)
     avg = ms / max(n, 1) * 1e-3
     peak_f = PEAK_TFLOPS[dtype]
     if fl / (peak_f * 1e12) >= by / (PEAK_HBM_GBS * 1e9):
@@ -240,6 +254,11 @@ def main():
     ap.add_argument("--f32-steps", type=int, default=3)
     ap.add_argument("--input", default="f32", choices=["u8", "f32"],
                     help="cell input: raw u8 clips (converted in-kernel) or the f32 tensor")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="N>1: BatchNorm statistics over all ranks' clips (SyncBN, opt-in)")
+    ap.add_argument("--no-grad-overlap", action="store_true",
+                    help="N>1: all-reduce every gradient after backward (default: the cell's "
+                         "early gradients on a side stream under the k x k weight-gradient kernel)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check on CPU (gloo), no GPU work")
     args = ap.parse_args()
@@ -247,7 +266,7 @@ def main():
     rc = launch_ranks(sys.argv[1:], args.gpus)
     if rc is not None:
         sys.exit(rc)
-    from ptamd.dist import GradBucket, env_rank
+    from ptamd.dist import CellDist, GradBucket, env_rank
     rank, local_rank, world = env_rank()
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
@@ -271,8 +290,11 @@ def main():
         if world > 1:                       # identical init on every rank
             for p in model.parameters():
                 dist.broadcast(p.data, 0)
-        return (model, GradBucket(model.parameters(), dev),
-                torch.optim.Adam(model.parameters(), lr=3e-4))
+        bucket = GradBucket(model.parameters(), dev)
+        if world > 1:
+            model.cell_dist = CellDist(sync_bn=args.sync_bn,
+                                       bucket=None if args.no_grad_overlap else bucket)
+        return model, bucket, torch.optim.Adam(model.parameters(), lr=3e-4)
 
     model, bucket, opt = build(args.dtype)
     crit = torch.nn.BCEWithLogitsLoss()
@@ -349,10 +371,11 @@ def main():
     if rank == 0:
         xb = 1 if args.input == "u8" else 4
         value = world * args.batch * args.steps / el
+        fused = kern["k_fused_fa"][1] > 0
         dom = max(kern, key=lambda k: kern[k][0])
         dom_ms, dom_n = kern[dom]
         roof, fl, by, avg_ms = kernel_roofline(dom, dom_ms, dom_n, args.batch, args.frames,
-                                               args.steps, args.dtype, xb)
+                                               args.steps, args.dtype, xb, fused)
         roof.update({"traffic": pmc_traffic(dom, args.batch, args.frames, args.dtype, version),
                      "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
                      "algorithmic_flop_per_launch": fl, "algorithmic_bytes_per_launch": by})
@@ -360,11 +383,11 @@ def main():
         # dominant one above): conv / wgrad are MFMA-bound, point-wise HBM-bound
         per_kind = {}
         for k, (ms, n) in kern.items():
-            if n == 0 or ms <= 0 or (algorithmic_flops(k, 1, args.frames) == 0 and
-                                     algorithmic_bytes(k, 1, args.frames, 2) == 0):
+            if n == 0 or ms <= 0 or (algorithmic_flops(k, 1, args.frames, fused) == 0 and
+                                     algorithmic_bytes(k, 1, args.frames, 2, 4, fused) == 0):
                 continue
             r, _, _, a = kernel_roofline(k, ms, n, args.batch, args.frames, args.steps,
-                                         args.dtype, xb)
+                                         args.dtype, xb, fused)
             per_kind[k] = {"bound": r["bound"], "achieved": r["achieved"], "unit": r["unit"],
                            "frac": r["frac"], "avg_launch_us": round(a * 1e3, 2)}
         line = {
@@ -384,7 +407,9 @@ def main():
                                    f"{args.batch} clips/GPU, {args.dtype} cell, {args.input} input",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "frames": args.frames, "channels": C, "kernel": K, "input": args.input,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "batchnorm": "sync" if (args.sync_bn and world > 1) else "per-replica",
+                       "grad_overlap": world > 1 and not args.no_grad_overlap},
             "roofline": roof,
             "roofline_per_kernel": per_kind,
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kern.items()},

@@ -921,10 +921,18 @@ __device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, size_t ro, int 
 
 // One image row of forward point-wise A (x of the row staged in xs, BN1 stats
 // of frame t-1 in stat[64..127]).
+// tile: the fused kernel's conv tile (bf16, 32x32 frames): gE_t of the row is
+// also written into its interior, rounded as the store rounds it.
+template <class S>
+__device__ __forceinline__ void tile_put_cl(S* tile, int y, int c, int h, const f32x16& v) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tile[tile_off<S, PADMAX>(y + PADMAX, cl_x(r, h) + PADMAX, c)] = (S)v[r];
+}
+
 template <class S, int ACT, int HG>
 __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
                                        int yl, float* wscr, int b, int y, size_t ro,
-                                       const FaIn<S>& in, int lane) {
+                                       const FaIn<S>& in, int lane, S* tile = nullptr) {
   using F = typename Tr<S>::frag;
   const int c = lane & 31, h = lane >> 5;
   const int t = a.t, T = a.T;
@@ -966,6 +974,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) gEv[r] = (float)(bf16_t)gEv[r];
   store_cl(a.gE + t * fs + ro, c, h, gEv);
+  if (tile) tile_put_cl(tile, y, c, h, gEv);
   if (a.gates && c < a.Cu) {
     const TileLoc tl = tile_loc(b, a.ntx, a.nty);
     const int W = a.ntx * IMG;
@@ -1045,7 +1054,7 @@ __device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, size_t ro, int 
 template <class S, int ACT, int HG>
 __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
                                        int yl, float* wscr, int y, size_t ro, const FbIn<S>& in,
-                                       int lane) {
+                                       int lane, S* tile = nullptr) {
   using F = typename Tr<S>::frag;
   const int c = lane & 31, h = lane >> 5;
   const size_t fs = fr_off(1, a.B);
@@ -1078,6 +1087,7 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) In[r] = (float)(bf16_t)In[r];
   store_cl(a.I + a.t * fs + ro, c, h, In);
+  if (tile) tile_put_cl(tile, y, c, h, In);
 }
 
 template <class S, int ACT, int HG>
@@ -1113,6 +1123,106 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   fb_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, y, ro, in, lane);
 }
 
+
+// =========================================================================
+// Fused forward segments (bf16, 32x32 frames, k <= 7): ONE workgroup per clip
+// (8 waves, 4 rows each) runs the point-wise step of all 32 rows and writes
+// the conv input straight into the LDS tile, then the k x k conv and its BN
+// partials -- one launch per BatchNorm segment instead of two, and the conv
+// never re-reads its input from HBM (the input is still stored: the backward
+// needs it).  Arithmetic identical to k_pw_fa / k_pw_fb + k_conv_fwd: the
+// tile holds the same bf16-rounded values the split conv would load.
+//   k_fused_fa(t): fa_row (close E_{t-1}; att, gE_t, eg_t) -> conv(gE_t, w_inh)
+//   k_fused_fb(t): fb_row (BN0, I_t)                        -> conv(I_t, w_exc)
+// LDS: conv tile | red | x of the clip frame | per-wave transpose scratch | stat
+// (the conv's B fragments come from L2 into registers: no weight slices).
+// =========================================================================
+constexpr int FUSED_NW = CONV_NT / 64, FUSED_RW = IMG / FUSED_NW;
+template <class S> constexpr int fused_lds_bytes() {
+  return tile_bytes<S, PADMAX>() + CONV_MISC * 4 + NPIX * 16 + FUSED_NW * SCR_FLOATS * 4 + 128 * 4;
+}
+struct FusedLds { char* tile; float* red; f32x4* xs; float* scr; float* stat; };
+template <class S>
+__device__ __forceinline__ FusedLds fused_carve(char* smem) {
+  FusedLds l;
+  l.tile = smem;
+  l.red = (float*)(smem + tile_bytes<S, PADMAX>());
+  l.xs = (f32x4*)(l.red + CONV_MISC);
+  l.scr = (float*)(l.xs + NPIX);
+  l.stat = l.scr + FUSED_NW * SCR_FLOATS;
+  return l;
+}
+
+// The conv half: conv(tile, wf) for this wave's rows, rows stored as they
+// finish (out_raw), then the per-clip BN partials (bnout).
+template <class S>
+__device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<S>& c, char* smem,
+                                           const FusedLds& L, int b, int wave, int lane, int tid) {
+  constexpr int RW = FUSED_RW;
+  f32x16 acc[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) acc[i] = zero16();
+  const int h = lane >> 5, px = lane & 31;
+  const StoreRow<S> sr{c.out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h};
+  auto nofill = [](int) {};                 // the point-wise half filled the tile
+  conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
+                                   tid, 0, sr);
+  bn_fwd_partial<RW, FUSED_NW>(acc, L.red, c.bnout, b, lane, wave, tid, 0,
+                               (int*)(smem + CONV_NT * 16), (double*)smem);
+}
+
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(CONV_NT, 1) void k_fused_fa(CellArgs<S> a, ConvArgs<S> c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const FusedLds L = fused_carve<S>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x, t = a.t;
+  if (wave == FUSED_NW - 1 && t > 0)
+    bn_fwd_finalize(bnf_src(a, t - 1, 1), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat + 64,
+                    b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
+  // this wave's first row's tiles go out before the staging and the barrier
+  FaIn<S> nxt = fa_load(a, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
+  tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
+  stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  __syncthreads();
+#pragma unroll 1
+  for (int i = 0; i < FUSED_RW; ++i) {
+    const int y = wave * FUSED_RW + i;
+    const size_t ro = clip_off(b) + (size_t)y * IMG * C;
+    const FaIn<S> cur = nxt;
+    if (i + 1 < FUSED_RW) nxt = fa_load(a, ro + (size_t)IMG * C, cl, h);   // next row in flight
+    fa_row<S, ACT, HG>(a, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
+                       (S*)L.tile);
+  }
+  fused_conv<S>(a, c, smem, L, b, wave, lane, tid);
+}
+
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(CONV_NT, 1) void k_fused_fb(CellArgs<S> a, ConvArgs<S> c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const FusedLds L = fused_carve<S>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x, t = a.t;
+  if (wave == FUSED_NW - 1)
+    bn_fwd_finalize(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
+                    b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
+  FbIn<S> nxt = fb_load<S, HG>(a, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
+  tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
+  stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  __syncthreads();
+#pragma unroll 1
+  for (int i = 0; i < FUSED_RW; ++i) {
+    const int y = wave * FUSED_RW + i;
+    const size_t ro = clip_off(b) + (size_t)y * IMG * C;
+    const FbIn<S> cur = nxt;
+    if (i + 1 < FUSED_RW) nxt = fb_load<S, HG>(a, ro + (size_t)IMG * C, cl, h);
+    fb_row<S, ACT, HG>(a, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
+                       (S*)L.tile);
+  }
+  fused_conv<S>(a, c, smem, L, b, wave, lane, tid);
+}
 
 // -------------------------------------------------------------------------
 // Backward point-wise A (t from T-1 down to -1).  Two halves:
@@ -2274,6 +2384,17 @@ void launch_pw(K kern, dim3 grid, size_t lds, hipStream_t st, const A& a) {
                    : launch_pw(kern<S, 0, 0>, grid, lds, st, a)))
 
 
+// (activation, cell) -> fused kernel instantiation: grid = clips, CONV_NT threads
+template <class K, class A, class Cv>
+void launch_fused(K kern, int nclip, size_t lds, hipStream_t st, const A& a, const Cv& c) {
+  hipLaunchKernelGGL(kern, dim3(nclip), dim3(CONV_NT), lds, st, a, c);
+}
+#define FUSED_LAUNCH(kern, c)                                                                \
+  (a.hgru ? (a.act ? launch_fused(kern<S, 1, 1>, p.B, fused_lds_bytes<S>(), st, a, c)         \
+                   : launch_fused(kern<S, 0, 1>, p.B, fused_lds_bytes<S>(), st, a, c))        \
+          : (a.act ? launch_fused(kern<S, 1, 0>, p.B, fused_lds_bytes<S>(), st, a, c)         \
+                   : launch_fused(kern<S, 0, 0>, p.B, fused_lds_bytes<S>(), st, a, c)))
+
 #define SETLDS(kern, bytes) \
   HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
 
@@ -2302,6 +2423,14 @@ int set_lds_attrs() {
   SETLDS((k_pw_fb<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
   SETLDS((k_pw_bb<S, 1, 1>), (pwb_lds_bytes<S>()));
+  SETLDS((k_fused_fa<S, 0, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fa<S, 0, 1>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fa<S, 1, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fa<S, 1, 1>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 0, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 0, 1>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 1, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 1, 1>), fused_lds_bytes<S>());
   SETLDS((k_wgrad<S, PADMAX>), (wgrad_lds_bytes<S, PADMAX>()));
   SETLDS((k_wgrad<S, PADBIG>), (wgrad_lds_bytes<S, PADBIG>()));
   done = true;
@@ -2345,6 +2474,21 @@ int bn_sync(const pt_cell_dist* dist, const double* grp, int ngrp, int nv, size_
   return 0;
 }
 inline bool syncbn(const pt_cell_dist* dist) { return dist && dist->bn_world > 1; }
+// The fused forward (k_fused_fa / k_fused_fb) covers the bf16 InT / hGRU cell
+// on single-tile (32x32) frames with k <= 7 and the inhibition branch; other
+// configurations, and PT_CELL_FUSED=0, run the split kernels.
+bool fused_env() {
+  static const bool on = [] {
+    const char* e = getenv("PT_CELL_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+bool use_fused(const pt_cell_desc* d, const Plan& p) {
+  return fused_env() && d->dtype == PT_DTYPE_BF16 && p.ntx * p.nty == 1 &&
+         p.K <= 2 * PADMAX + 1 && !d->no_inh;
+}
+
 int check_dist(const pt_cell_dist* dist) {
   if (!dist) return 0;
   if (dist->bn_world < 1) return fail(PT_ERR_ARG, "bn_world must be >= 1%s (got %ld)", "", dist->bn_world);
@@ -2386,6 +2530,21 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
   ca.wf = a.wf_inh;
   cb.wf = a.wf_exc;
+  if (use_fused(d, p)) {        // one launch per BatchNorm segment (k_fused_fa / k_fused_fb)
+    for (int t = 0; t < p.T; ++t) {
+      a.t = t;
+      ca.out_raw = a.ci + t * fs; ca.bnout = bnf_slot(a, t, 0);
+      timed(PT_K_FUSED_FA, st, [&] { FUSED_LAUNCH(k_fused_fa, ca); });
+      if (syncbn(dist))
+        if (int rc = bn_sync(dist, ca.bnout.grp, bn_ngrp(p.B), 96, ((size_t)t * 2 + 0) * 96, st)) return rc;
+      cb.out_raw = a.ce + t * fs; cb.bnout = bnf_slot(a, t, 1);
+      timed(PT_K_FUSED_FB, st, [&] { FUSED_LAUNCH(k_fused_fb, cb); });
+      if (syncbn(dist))
+        if (int rc = bn_sync(dist, cb.bnout.grp, bn_ngrp(p.B), 96, ((size_t)t * 2 + 1) * 96, st)) return rc;
+    }
+    a.t = p.T;
+    timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });     // closes E_{T-1}
+  } else
   for (int t = 0; t <= p.T; ++t) {
     a.t = t;
     timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });

@@ -35,7 +35,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from ptamd.dist import GradBucket, env_rank, lockstep  # noqa: E402
+from ptamd.dist import CellDist, GradBucket, env_rank, lockstep  # noqa: E402
 from utils import engine  # noqa: E402
 from utils.earlystopping import EarlyStopping  # noqa: E402
 from utils.misc_functions import AverageMeter, acc_scores  # noqa: E402
@@ -161,6 +161,9 @@ def main(argv=None):
             dist.broadcast(p.data, 0)
     print("Loading finished" if world == 1 else f"data-parallel over {world} ranks")
     bucket = GradBucket(model.parameters(), device)
+    if world > 1 and hasattr(model, "cell_dist") and device.type == "cuda":
+        model.cell_dist = CellDist(sync_bn=args.sync_bn,
+                                   bucket=None if args.no_grad_overlap else bucket)
     # HIP-cell models take the raw u8 clips: the /255 conversion and the
     # [B,T,H,W,3] -> [B,3,T,H,W] transpose happen while the kernels stage x
     keep_u8 = getattr(model, 'accepts_u8', False) and not args.f32_input

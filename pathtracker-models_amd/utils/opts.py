@@ -60,3 +60,9 @@ parser.add_argument('--results-root', type=str, default=None)
 parser.add_argument('--max-iters', type=int, default=0)
 parser.add_argument('--f32-input', default=False, action='store_true',
                     help='hand the HIP-cell models the f32 [B,3,T,H,W] tensor instead of the raw u8 clips')
+parser.add_argument('--sync-bn', default=False, action='store_true',
+                    help='HIP-cell models, several ranks: BatchNorm statistics over every rank\'s clips '
+                         '(SyncBN) instead of per replica as the reference\'s DataParallel')
+parser.add_argument('--no-grad-overlap', default=False, action='store_true',
+                    help='several ranks: average every gradient after backward instead of the cell\'s '
+                         'early gradients on a side stream under the k x k weight-gradient kernel')

@@ -1,0 +1,69 @@
+"""The fused forward (k_fused_fa / k_fused_fb: the point-wise step of a clip's
+32 rows and the k x k conv in ONE launch per BatchNorm segment, bf16, 32 x 32
+frames) against the split kernels (k_pw_fa, k_conv_fwd, k_pw_fb, k_conv_fwd):
+the arithmetic is the same operation for operation (the LDS tile holds the
+bf16 values the split conv would load), so logits, per-frame testmode outputs
+and every gradient must agree bit for bit.  PT_CELL_FUSED=0 selects the split
+path (read per call by the library)."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def _run(m, x, y, fused):
+    os.environ["PT_CELL_FUSED"] = "1" if fused else "0"
+    try:
+        m.zero_grad(set_to_none=True)
+        out, _ = m(x)
+        F.binary_cross_entropy_with_logits(out, y.reshape(-1, 1)).backward()
+        with torch.no_grad():
+            lo, states, gates = m(x, testmode=True)
+        torch.cuda.synchronize()
+        return (out.detach().clone(), states.clone(), gates.clone(),
+                {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None})
+    finally:
+        os.environ.pop("PT_CELL_FUSED", None)
+
+
+@pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("int", "tanh", 5, 3),
+                                          ("hgru", "softplus", 16, 6), ("int", "softplus", 256, 64)])
+def test_fused_forward_is_bitwise_the_split_forward(cell, act, b, t):
+    from models import InT, ffhgru_hierarchy as hg
+    from ptamd import synth
+    dev = _dev()
+    torch.manual_seed(b + t)
+    if cell == "hgru":
+        m = hg.FFhGRU(dimensions=32, timesteps=t, kernel_size=7)
+    else:
+        m = InT.InT(dimensions=32, timesteps=t, kernel_size=7,
+                    nl=torch.tanh if act == "tanh" else F.softplus)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
+                p.uniform_(0.5, 1.5)
+            elif n.endswith(("mu", "gamma")):
+                p.uniform_(-0.5, 0.5)
+    m = m.to(dev)
+    m.cell_dtype = "bf16"
+    clips, labels = synth.make_batch(b * 7 + t, b, t)
+    x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float().to(dev)
+    y = torch.tensor([ord(v) for v in labels], dtype=torch.float32, device=dev)
+    o1, s1, g1, gr1 = _run(m, x, y, fused=True)
+    o0, s0, g0, gr0 = _run(m, x, y, fused=False)
+    assert torch.isfinite(o1).all()
+    assert torch.equal(o1, o0) and torch.equal(s1, s0) and torch.equal(g1, g0)
+    for k in gr0:
+        if k.startswith(("unit1.", "preproc.")):      # the library's gradients: bitwise
+            assert torch.equal(gr1[k], gr0[k]), k
+        else:                                          # readout (MIOpen): same inputs
+            torch.testing.assert_close(gr1[k], gr0[k], rtol=1e-5, atol=1e-8)

@@ -21,7 +21,8 @@ T=64 frames, bf16 cell) and the 64-frame recurrence in exact arithmetic.
   for bit and the capture and its replays must reproduce them bit for bit:
   any buffer read before it is (re)written would show up as a difference.
 
-The measured errors are written to gpurun_out/headline_parity.json.
+The measured errors are written to gpurun_out/parity_records.json (tests/goldens.py
+record; copied into profiles/ by tools/collect_profiles.py).
 """
 import ctypes
 import json
@@ -45,12 +46,8 @@ def _dev():
 
 
 def _record(key, val):
-    d = os.path.join(REPO, "gpurun_out")
-    os.makedirs(d, exist_ok=True)
-    p = os.path.join(d, "headline_parity.json")
-    cur = json.load(open(p)) if os.path.exists(p) else {}
-    cur[key] = val
-    json.dump(cur, open(p, "w"), indent=1)
+    from goldens import record
+    record(key, val)
 
 
 def _model(seed, perturb, t=T):

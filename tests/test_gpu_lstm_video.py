@@ -143,8 +143,6 @@ def test_bf16_matches_f32_at_cfg3_size():
     against the f32 cell (itself pinned to the oracle above) on the bench's
     clips — logits within 5e-2, identical 0.5 / 0 decisions for every clip
     farther than that from the threshold, per-tensor gradient cosine >= 0.99."""
-    import json
-    import os
     from models import convlstm
     dev = _dev()
     x, y = _clips(1000, 256, 64)
@@ -174,9 +172,8 @@ def test_bf16_matches_f32_at_cfg3_size():
     rec = {"logit_max_abs_err": err, "logit_spread": float(o32.max() - o32.min()),
            "grad_cosine_min": min(cos.values()), "grad_cosine_min_tensor": min(cos, key=cos.get),
            "flips_away_from_threshold": flips}
-    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
-    os.makedirs(d, exist_ok=True)
-    json.dump(rec, open(os.path.join(d, "convlstm_video_parity.json"), "w"), indent=1)
+    from goldens import record
+    record("convlstm_video_bf16_vs_f32_B256_T64", rec)
     assert err <= tol, rec
     assert flips == {"train_0.5": 0, "eval_0": 0}, rec
     bad = {n: v for n, v in cos.items() if v < 0.99}
