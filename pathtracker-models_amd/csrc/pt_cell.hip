@@ -39,19 +39,29 @@ enum SmallSlot {
 constexpr int SLAB_G = 6 * 1024;                 // 6 gate weights [n][ci]
 constexpr int SLAB = SLAB_G + NSMALL * 32;
 constexpr int NTRANS = 12;                       // backward transients incl. dAt, GEfin
-// BatchNorm batch sums, bitwise reproducible (no floating-point atomics):
-// every producer (forward: the conv workgroup of one clip / tile; backward: a
-// point-wise workgroup) stores its partial sums in its own slot; the last
-// producer to arrive in its group of bn_gsize() (an arrival ticket: stores
-// drained, agent-scope release, one relaxed agent-scope counter add, the last
-// arriver acquires) adds the group's partials in slot order and stores the
-// group sum; a consumer adds the <= NGRP group sums in group order.  Every
-// sum therefore has one fixed association, whatever the dispatch order or
-// the XCD placement: runs, and hipGraph replays, agree bit for bit.
+// BatchNorm batch sums.  PT_BN_MODE selects the reduction (compile time):
+//  2 (default) bitwise reproducible, no floating-point atomics: every producer
+//    (forward: the conv workgroup of one clip / tile; backward: a point-wise
+//    workgroup) stores its 64 partial sums in its own slot with write-through
+//    (sc1) stores, its wave 0 drains them and takes an arrival ticket (one
+//    relaxed agent-scope vector atomic; no release fence, so no L2 write-back);
+//    the last producer to arrive in its group of bn_gsize() adds the group's
+//    partials in slot order, reading them with sc1 loads (never a stale L1
+//    line), and stores the group sum; a consumer adds the <= NGRP group sums in
+//    group order.  Every sum has one fixed association, whatever the dispatch
+//    order or XCD placement: runs and hipGraph replays agree bit for bit.
+//  1 the same ticket with plain stores + an agent-scope release / acquire
+//    fence pair (measured: the per-workgroup release, an L2 write-back, made
+//    k_pw_bb 2x slower).
+//  0 fp64 atomics into NGRP copies (order-dependent rounding).
+#ifndef PT_BN_MODE
+#define PT_BN_MODE 2
+#endif
 constexpr int NGRP = 16;
 constexpr int BNB_WG_PER_CLIP = 8;     // backward producers per clip at most (PW_PARTS)
 __host__ __device__ inline int bn_gsize(int nprod) { return (nprod + NGRP - 1) / NGRP; }
 __host__ __device__ inline int bn_ngrp(int nprod) {
+  if (PT_BN_MODE == 0) return NGRP;    // copies, all read (unused ones stay zero)
   const int g = bn_gsize(nprod);
   return (nprod + g - 1) / g;
 }
@@ -62,27 +72,8 @@ struct BnSlot {       // one (frame, BatchNorm) reduction
   int nprod;          // producers in the launch
 };
 
-// Arrival ticket (all threads call it after storing their partials): every
-// wave drains its stores, one lane releases at agent scope and takes a ticket
-// with one relaxed agent-scope vector atomic; the group's last arriver
-// acquires (drops this CU's L1) and every thread of it gets true.  flag: an
-// LDS word no other code touches until the caller's next barrier.
-__device__ __forceinline__ bool bn_arrive(unsigned* cnt, int nmem, int tid, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (unsigned)(nmem - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0;
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The last arriver of group g: sums of the group's partials in slot order, fp64.
@@ -98,7 +89,8 @@ __device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
   double a = 0.0, b = 0.0;
 #pragma unroll 8
   for (int m = m0 + q; m < m1; m += Q) {
-    const double x = (double)s.part[(size_t)m * 64 + v];
+    const float* pp = s.part + (size_t)m * 64 + v;
+    const double x = (double)(PT_BN_MODE == 2 ? ld_sc1(pp) : *pp);
     a += x;
     b += x * x;
   }
@@ -123,15 +115,54 @@ __device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
   }
 }
 
-// Producer side: this workgroup's 64 partial values (lanes tid < 64 hold
-// value tid) into slot `prod`, the ticket, and the group sum if last.
+// Producer side: this workgroup's 64 partial values (lanes tid < 64 -- wave 0
+// -- hold value tid) into the reduction.  All threads call it.  flag: an LDS
+// word no other code touches until the caller's next barrier; scr: see
+// bn_group_sum.
 template <int NTH, bool FWD>
 __device__ __forceinline__ void bn_publish(const BnSlot& s, int prod, float val, int tid, int* flag,
                                            double* scr) {
-  if (tid < 64) s.part[(size_t)prod * 64 + tid] = val;
+#if PT_BN_MODE == 0
+  if (tid < 64) {
+    double* o = s.grp + (size_t)(prod % NGRP) * (FWD ? 96 : 64);
+    const double d = (double)val;
+    if (FWD && tid < 32) { unsafeAtomicAdd(o + tid, d); unsafeAtomicAdd(o + 32 + tid, d * d); }
+    else unsafeAtomicAdd(o + (FWD ? 32 : 0) + tid, d);
+  }
+  (void)flag; (void)scr;
+#else
   const int G = bn_gsize(s.nprod), g = prod / G;
   const int nmem = min(G, s.nprod - g * G);
-  if (bn_arrive(s.cnt + g, nmem, tid, flag)) bn_group_sum<NTH, FWD>(s, g, tid, scr);
+  if (tid < 64) {
+#if PT_BN_MODE == 2
+    __hip_atomic_store(s.part + (size_t)prod * 64 + tid, val, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);                  // write-through
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this wave's payload is in L2
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(s.cnt + g, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      *flag = old == (unsigned)(nmem - 1);
+    }
+#else
+    s.part[(size_t)prod * 64 + tid] = val;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(s.cnt + g, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == (unsigned)(nmem - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+#endif
+  }
+  __syncthreads();
+  if (*flag) bn_group_sum<NTH, FWD>(s, g, tid, scr);
+#endif
 }
 
 // ----------------------------------------------------------------- arguments
@@ -2301,14 +2332,15 @@ Plan plan(const pt_cell_desc* d) {
   p.saved = o;
   o = 0;
   // tickets first (the only words cleared per call), then partials and group sums
-  p.bnf_cnt_bytes = al((size_t)p.T * 2 * NGRP * 4);
-  p.o_bnf_cnt = o; o += p.bnf_cnt_bytes;
-  p.o_bnf_part = o; o += al((size_t)p.T * 2 * p.B * 64 * 4);
+  // (PT_BN_MODE 0 accumulates into the group sums: they are cleared too)
+  p.o_bnf_cnt = o; o += al((size_t)p.T * 2 * NGRP * 4);
   p.o_bnf_grp = o; o += al((size_t)p.T * 2 * NGRP * 96 * 8);
-  p.bnb_cnt_bytes = al((size_t)p.T * 2 * NGRP * 4);
-  p.o_bnb_cnt = o; o += p.bnb_cnt_bytes;
-  p.o_bnb_part = o; o += al((size_t)p.T * 2 * p.B * BNB_WG_PER_CLIP * 64 * 4);
+  p.bnf_cnt_bytes = PT_BN_MODE == 0 ? o - p.o_bnf_cnt : p.o_bnf_grp - p.o_bnf_cnt;
+  p.o_bnf_part = o; o += al((size_t)p.T * 2 * p.B * 64 * 4);
+  p.o_bnb_cnt = o; o += al((size_t)p.T * 2 * NGRP * 4);
   p.o_bnb_grp = o; o += al((size_t)p.T * 2 * NGRP * 64 * 8);
+  p.bnb_cnt_bytes = PT_BN_MODE == 0 ? o - p.o_bnb_cnt : p.o_bnb_grp - p.o_bnb_cnt;
+  p.o_bnb_part = o; o += al((size_t)p.T * 2 * p.B * BNB_WG_PER_CLIP * 64 * 4);
   for (int i = 0; i < NTRANS; ++i) { p.o_tr[i] = o; o += al(p.frame * 4); }   // GEfin f32
   p.o_dci = o; o += fbytes;
   p.o_dce = o; o += fbytes;

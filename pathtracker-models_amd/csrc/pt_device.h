@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace ptc {
 
 constexpr int C = 32;          // channels (MFMA tile width)
@@ -433,7 +435,12 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
 // column kw+1 is fetched from L2 into registers at the top of column kw and
 // written to LDS after its MFMAs, so no MFMA ever waits on an L2 round trip
 // and each workgroup reads the weights once instead of once per wave.
-constexpr int CONV_PF = 3;          // A-fragment prefetch depth (tile rows)
+#ifndef CONV_PF
+#define CONV_PF 3                    // A-fragment prefetch depth (tile rows)
+#endif
+#ifndef PT_CONV_FLAT
+#define PT_CONV_FLAT 0               // 1: one (column, row) pipeline for the register-weight convs
+#endif
 constexpr int WSLICE_CHUNKS = 896;   // 16-B chunks per slice: 7 taps x 2 x 64 x 16 B (bf16)
                                      //                       = 7 taps x 8 x 64 x 4 B (f32, per pass)
 constexpr int WSLICE_BYTES = WSLICE_CHUNKS * 16;
@@ -496,6 +503,17 @@ struct NoRowHook {
   static constexpr bool wreg = false;
 };
 
+// Compile-time loop: fn(std::integral_constant<int, I>) for I in [I0, N), so
+// every register-array index derived from I is a constant (a #pragma unroll
+// the compiler declines would leave dynamic indices, i.e. scratch).
+template <int I, int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  if constexpr (I < N) {
+    fn(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(fn);
+  }
+}
+
 // k > 7 (PAD = PADBIG): the 46 x 46 tile leaves no LDS for weight slices;
 // every wave reads its column's K x KSP B fragments straight from L2 at the
 // top of the column (the ~K * RPW * KSP MFMAs of the column cover the fetch).
@@ -515,6 +533,112 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
   constexpr int off = PAD - K / 2;
   constexpr int NTR = RW + K - 1;           // tile rows touched by this wave
   const int h = lane >> 5, px = lane & 31;
+#if PT_CONV_FLAT
+  // One software pipeline over all (column, tile row) steps: the A fragments
+  // run CONV_PF steps ahead ACROSS column boundaries too (the per-column
+  // loop below drains its prefetch at the end of every column), and the
+  // column fragments alternate between two register sets (no copies).
+  if constexpr (WREG && TT::NPASS == 1) {
+    F bw[2][K][KSP];
+    auto load_colw = [&](int kw, F (&dst)[K][KSP]) {
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+        for (int s = 0; s < KSP; ++s) dst[kh][s] = wf[((kh * K + kw) * TT::KS + s) * 64 + lane];
+    };
+    load_colw(0, bw[0]);
+    __syncthreads();
+    if (!(ablate & 2)) fill(0);
+    __syncthreads();
+    if (ablate & 1) return;
+    constexpr int NST = K * NTR;
+    constexpr int PF = CONV_PF < NST ? CONV_PF : NST;
+    F av[PF + 1][KSP];
+    auto load_step = [&](int st) {
+      const int kw = st / NTR, tr = st - kw * NTR;
+      const int trow = row0 + tr + off, tcol = px + kw + off;
+#pragma unroll
+      for (int s = 0; s < KSP; ++s)
+        av[st % (PF + 1)][s] = *(const F*)(tile + tile_off<S, PAD>(trow, tcol, 16 * s + 8 * h));
+    };
+    static_for<0, PF>([&](auto c) { load_step(decltype(c)::value); });
+    static_for<0, NST>([&](auto c) {
+      constexpr int st = decltype(c)::value;
+      constexpr int kw = st / NTR, tr = st - kw * NTR;
+      if constexpr (tr == 0) {
+        if constexpr (kw + 1 < K) load_colw(kw + 1, bw[(kw + 1) & 1]);
+        if constexpr (Done::prefetch_active && kw == 0) done.prefetch();
+      }
+      if constexpr (st + PF < NST) load_step(st + PF);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < KSP; ++s)
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh) {
+          const int i = tr - kh;
+          if (i >= 0 && i < RW) acc[i] = TT::mma(bw[kw & 1][kh][s], av[st % (PF + 1)][s], acc[i]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (Done::active && kw == K - 1 && tr >= K - 1 && tr - (K - 1) < RW)
+        done(tr - (K - 1), acc[tr - (K - 1)]);
+    });
+    return;
+  }
+  // the LDS slice ring (k <= 7 without register weights: the backward convs),
+  // same single pipeline: the A fragments of the next column are in flight
+  // across the column's slice hand-off barrier
+  if constexpr (LDSW && TT::NPASS == 1) {
+    WSlice pre;
+    wslice_load<S, K, NTH>(pre, wf, 0, 0, tid);
+    __syncthreads();
+    if (!(ablate & 2)) fill(0);
+    wslice_store<K, NTH>(pre, wbuf, tid);
+    __syncthreads();
+    if (ablate & 1) return;
+    constexpr int NST = K * NTR;
+    constexpr int PF = CONV_PF < NST ? CONV_PF : NST;
+    F av[PF + 1][KSP];
+    F bc[K][KSP];
+    auto load_step = [&](int st) {
+      const int kw = st / NTR, tr = st - kw * NTR;
+      const int trow = row0 + tr + off, tcol = px + kw + off;
+#pragma unroll
+      for (int s = 0; s < KSP; ++s)
+        av[st % (PF + 1)][s] = *(const F*)(tile + tile_off<S, PAD>(trow, tcol, 16 * s + 8 * h));
+    };
+    static_for<0, PF>([&](auto c) { load_step(decltype(c)::value); });
+    static_for<0, NST>([&](auto c) {
+      constexpr int st = decltype(c)::value;
+      constexpr int kw = st / NTR, tr = st - kw * NTR;
+      if constexpr (tr == 0) {
+        if constexpr (kw > 0) {                 // publish column kw's slice
+          wslice_store<K, NTH>(pre, wbuf + (kw & 1) * WSLICE_BYTES, tid);
+          __syncthreads();
+        }
+        const F* wl = (const F*)(wbuf + (kw & 1) * WSLICE_BYTES) + lane;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+          for (int s = 0; s < KSP; ++s) bc[kh][s] = wl[(kh * KSP + s) * 64];
+        if constexpr (kw + 1 < K) wslice_load<S, K, NTH>(pre, wf, 0, kw + 1, tid);
+        if constexpr (Done::prefetch_active && kw == 0) done.prefetch();
+      }
+      if constexpr (st + PF < NST) load_step(st + PF);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < KSP; ++s)
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh) {
+          const int i = tr - kh;
+          if (i >= 0 && i < RW) acc[i] = TT::mma(bc[kh][s], av[st % (PF + 1)][s], acc[i]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (Done::active && kw == K - 1 && tr >= K - 1 && tr - (K - 1) < RW)
+        done(tr - (K - 1), acc[tr - (K - 1)]);
+    });
+    return;
+  }
+#endif
   F bn[K][KSP];                             // WREG: the next column's fragments
   auto load_col = [&](int pass, int kw) {
 #pragma unroll

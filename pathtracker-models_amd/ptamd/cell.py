@@ -192,7 +192,7 @@ class RecurrentCellFn(torch.autograd.Function):
         d_e_last = d_e_last.contiguous().float()
         ws = torch.empty(lib.pt_cell_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                          device=x.device)
-        need = list(ctx.needs_input_grad[3:])
+        need = list(ctx.needs_input_grad[4:])      # after x, cfg, want_seq, cdist
         if ctx.cfg.no_inh:
             need = [n and PARAM_KEYS[i] not in _UNUSED_NO_INH for i, n in enumerate(need)]
         grads = [torch.empty_like(p) if (p is not None and need[i]) else None

@@ -210,7 +210,7 @@ class LSTMStepsFn(torch.autograd.Function):
         ws = torch.empty(lib.pt_lstm_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                          device=dev)
         need = ctx.needs_input_grad
-        grads = [torch.empty(s, device=dev) if need[8 + i] else None
+        grads = [torch.empty(s, device=dev) if need[9 + i] else None      # weights follow 9 args
                  for i, s in enumerate(ctx.wshapes)]
         dx = torch.empty(xshape, device=dev) if need[0] else None
         dh0 = torch.empty((b, ch, hh, ww), device=dev) if (has_h0 and need[1]) else None

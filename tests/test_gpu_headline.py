@@ -2,13 +2,21 @@
 T=64 frames, bf16 cell) and the 64-frame recurrence in exact arithmetic.
 
 * bf16 vs f32 at B=256, T=64: the f32 HIP path is pinned to the reference at
-  1e-3 (test_gpu_parity.py goldens; the oracle at T=64 below), so at sizes the
-  CPU oracle cannot reach it is the reference.  Asserted: logits within
+  1e-3 (test_gpu_parity.py goldens; the oracle below), so at sizes the
+  CPU oracle cannot reach quickly it is the reference.  Asserted: logits within
   BF16_LOGIT_TOL; train (> 0.5, misc_functions.py:41) and eval (> 0,
   test_model.py:127) decisions identical for every clip whose f32 logit is
   farther than BF16_LOGIT_TOL from the threshold; per-tensor gradient cosine
-  >= 0.99.  Run on the bench's own init (seed 1234) and on parameters moved
-  off init (at init every logit is within 1e-2 of -0.265).
+  >= 0.99.  Run on the bench's own init (seed 1234), on parameters moved off
+  init, and on parameters trained for 300 bf16 steps on the bench's clips
+  (tests/golden/int_trained_headline.npz, tools/probe_headline.py --steps 300
+  --lr 2e-3).
+* final classification accuracy at the headline size in exact arithmetic: the
+  trained parameters with the readout's Linear(1,1) rescaled so that the 256
+  logits span 4 units around 0.25 (>= 25 % of the clips on each side of both
+  thresholds): f32 HIP vs the CPU oracle on the same clips -- logits within
+  1e-3 and every train / eval decision identical; bf16 vs f32 there: no flip
+  outside the rescaled bf16 band (the rescale multiplies the bf16 error).
 * f32 HIP vs the CPU oracle at T=64, B=8: logits 1e-3, every gradient
   1e-6 + 1e-3 max|g|.
 * hipGraph replay with poisoned buffers at B=256, T=64, bf16 (the config of
@@ -35,7 +43,9 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 B, T = 256, 64
-BF16_LOGIT_TOL = 5e-2
+# bf16 vs f32 logit bound at B=256, T=64: measured 6.8e-4 (perturbed init),
+# 2.2e-3 (trained 300 steps; profiles/r03_parity_records.json)
+BF16_LOGIT_TOL = 2.5e-3
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -50,8 +60,19 @@ def _record(key, val):
     record(key, val)
 
 
+def _trained(t=T):
+    """InT with the parameters of tests/golden/int_trained_headline.npz."""
+    from goldens import load, params
+    from models import InT
+    m = InT.InT(dimensions=32, timesteps=t, kernel_size=7)
+    m.load_state_dict(params(load("int_trained_headline")), strict=True)
+    return m
+
+
 def _model(seed, perturb, t=T):
     from models import InT
+    if perturb == "trained":
+        return _trained(t)
     torch.manual_seed(seed)
     m = InT.InT(dimensions=32, timesteps=t, kernel_size=7)
     if perturb:
@@ -77,7 +98,7 @@ def _run(m, dtype, x, y):
              if p.grad is not None})
 
 
-@pytest.mark.parametrize("perturb", [False, True])
+@pytest.mark.parametrize("perturb", [False, True, "trained"])
 def test_bf16_matches_f32_at_headline_config(perturb):
     import bench
     dev = _dev()
@@ -101,12 +122,55 @@ def test_bf16_matches_f32_at_headline_config(perturb):
     stats["flips_away_from_threshold"] = flips
     stats["grad_cosine_min"] = min(cos.values())
     stats["grad_cosine_min_tensor"] = min(cos, key=cos.get)
-    _record(f"bf16_vs_f32_B{B}_T{T}_{'perturbed' if perturb else 'init'}", stats)
+    tag = perturb if isinstance(perturb, str) else ("perturbed" if perturb else "init")
+    _record(f"bf16_vs_f32_B{B}_T{T}_{tag}", stats)
     assert torch.isfinite(lo16).all()
     assert stats["logit_max_abs_err"] <= BF16_LOGIT_TOL, stats
     assert flips == {"train_0.5": 0, "eval_0": 0}, stats
     bad = {k: v for k, v in cos.items() if v < 0.99}
     assert not bad, f"gradient cosine < 0.99: {bad}"
+
+
+@pytest.mark.timeout(600)
+def test_headline_accuracy_f32_bit_identical_to_oracle():
+    """B=256, T=64, logits straddling both thresholds: f32 HIP == CPU oracle
+    decisions for every clip (north_star: final accuracy bit-identical)."""
+    import bench
+    from oracle import cells
+    dev = _dev()
+    x, y = bench.make_data(1000, B, T, torch.device("cpu"))
+    m = _trained().to(dev)
+    m.cell_dtype = "f32"
+    with torch.no_grad():
+        lo0 = m(x.to(dev))[0].double().flatten().cpu()
+        w0, b0 = float(m.readout_dense.weight), float(m.readout_dense.bias)
+        s = (lo0 - b0) / w0                               # the pooled readout feature
+        k = 4.0 / float(s.max() - s.min())               # logits span 4 units ...
+        m.readout_dense.weight.fill_(k)
+        m.readout_dense.bias.fill_(0.25 - k * float(s.median()))   # ... around 0.25
+        lo32 = m(x.to(dev))[0].double().flatten().cpu()
+        m.cell_dtype = "bf16"
+        lo16 = m(x.to(dev))[0].double().flatten().cpu()
+        sd = {n: p.detach().cpu() for n, p in m.named_parameters()}
+        ref = cells.recurrent_forward(sd, x)[0].double().flatten()
+    err = float((lo32 - ref).abs().max())
+    band16 = BF16_LOGIT_TOL * abs(k / w0)                 # the rescale scales the bf16 error
+    rec = {"logit_spread": float(ref.max() - ref.min()), "f32_vs_oracle_max_abs": err,
+           "readout_scale": k / w0, "bf16_band": band16,
+           "bf16_vs_f32_max_abs": float((lo16 - lo32).abs().max())}
+    for name, thr in (("train_0.5", 0.5), ("eval_0", 0.0)):
+        far = (ref - thr).abs() > 1e-3
+        rec[f"f32_flips_{name}"] = int(((lo32 > thr) != (ref > thr))[far].sum())
+        rec[f"undecided_1e-3_{name}"] = int((~far).sum())
+        rec[f"above_{name}"] = int((ref > thr).sum())
+        far16 = (lo32 - thr).abs() > band16
+        rec[f"bf16_flips_{name}"] = int(((lo16 > thr) != (lo32 > thr))[far16].sum())
+        rec[f"bf16_in_band_{name}"] = int((~far16).sum())
+    _record("headline_accuracy_B256_T64_trained_rescaled", rec)
+    assert err <= 1e-3, rec
+    for thr in ("train_0.5", "eval_0"):
+        assert rec[f"f32_flips_{thr}"] == 0 and rec[f"bf16_flips_{thr}"] == 0, rec
+        assert 0.25 * B <= rec[f"above_{thr}"] <= 0.75 * B, rec     # straddles the threshold
 
 
 def test_f32_matches_oracle_over_64_frames():

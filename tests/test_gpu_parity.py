@@ -104,18 +104,29 @@ def test_bptt_grads_and_adam_f32(tag):
         _assert_close(f"adam {k}", p.detach().cpu(), g["adam." + k], 1e-6, 1e-3)
 
 
+# bf16 cell vs the reference goldens (perturbed parameters, up to 32 frames):
+# the measured errors are recorded (gpurun_out/parity_records.json)
+BF16_GOLDEN_TOL = 2e-2
+
+
 @pytest.mark.parametrize("tag", ["int_c32", "int_cfg1", "hgru_c32", "hgru_64"])
 def test_forward_bf16_tolerance(tag):
-    """bf16 operands / saved states, f32 accumulation: logits within 5e-2 and
-    per-frame states within 5e-2 of the reference after up to 32 recurrent steps."""
+    """bf16 operands / saved states, f32 accumulation: logits within
+    BF16_GOLDEN_TOL and per-frame states within BF16_GOLDEN_TOL (absolute +
+    relative to max|state|) of the reference after up to 32 recurrent steps."""
     dev = _dev()
     g = load(tag)
     m = _model(g, "bf16").to(dev)
     x, _ = prepared_input(g)
     with torch.no_grad():
         logits, states, _ = m(x.to(dev), testmode=True)
-    _assert_close("bf16 logits", logits.cpu(), g["logits"], 5e-2)
-    _assert_close("bf16 states", states.cpu(), g["states"], 5e-2, 5e-2)
+    from goldens import record
+    lerr, _ = _err(logits.cpu(), g["logits"])
+    serr, sscale = _err(states.cpu(), g["states"])
+    record(f"bf16_vs_reference_{tag}", {"logit_max_abs_err": lerr, "state_max_abs_err": serr,
+                                        "state_max_abs": sscale})
+    _assert_close("bf16 logits", logits.cpu(), g["logits"], BF16_GOLDEN_TOL)
+    _assert_close("bf16 states", states.cpu(), g["states"], BF16_GOLDEN_TOL, BF16_GOLDEN_TOL)
 
 
 @pytest.mark.parametrize("tag", ["int_c32", "hgru_c32"])

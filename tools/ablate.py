@@ -31,6 +31,8 @@ def main():
     lib = _lib.load()
     kinds = [k for k in _lib.KIND_NAMES if k not in ("k_prep", "k_reduce")]
     res = {mk: {k: [] for k in kinds} for mk in masks}
+    tot = {mk: {"fwd": [], "bwd": [], "all": []} for mk in masks}     # summed device ms per step
+    fwd_kinds = {"k_pw_fa", "k_conv_fa", "k_pw_fb", "k_conv_fb", "k_fused_fa", "k_fused_fb"}
     for r in range(rounds + 1):
         for mk in masks:
             bits, _, env = mk.partition(":")
@@ -48,10 +50,15 @@ def main():
                 os.environ.pop(k)
             if r == 0:
                 continue
-            for name in kinds:
+            sums = {"fwd": 0.0, "bwd": 0.0, "all": 0.0}
+            for name in _lib.KIND_NAMES:
                 ms, n = _lib.timing_read(_lib.KIND_NAMES.index(name))
-                if n:
+                if n and name in kinds:
                     res[mk][name].append(1e3 * ms / n)
+                sums["all"] += ms
+                sums["fwd" if name in fwd_kinds else "bwd"] += ms
+            for k, v in sums.items():
+                tot[mk][k].append(v)
     os.environ.pop("PT_CELL_ABLATE")
     print(f"avg launch us (B={b} T={t} {dtype}), median of {rounds} rounds")
     print("mask  " + "  ".join(f"{k[2:]:>8}" for k in kinds))
@@ -61,6 +68,10 @@ def main():
             v = sorted(res[mk][k])
             row.append(f"{v[len(v) // 2]:8.1f}" if v else " " * 8)
         print(f"{mk:>4}  " + "  ".join(row))
+    print("summed device ms per step (median): " + "; ".join(
+        f"{mk}: fwd {sorted(tot[mk]['fwd'])[len(tot[mk]['fwd']) // 2]:.3f} "
+        f"bwd {sorted(tot[mk]['bwd'])[len(tot[mk]['bwd']) // 2]:.3f} "
+        f"all {sorted(tot[mk]['all'])[len(tot[mk]['all']) // 2]:.3f}" for mk in masks))
 
 
 if __name__ == "__main__":
