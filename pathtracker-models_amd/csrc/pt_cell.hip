@@ -57,6 +57,15 @@ constexpr int NTRANS = 12;                       // backward transients incl. dA
 #ifndef PT_BN_MODE
 #define PT_BN_MODE 2
 #endif
+#ifndef PT_SLAB_DMA
+#define PT_SLAB_DMA 1     // slab prefetch by LDS-DMA (0: through registers)
+#endif
+#ifndef PT_SLAB_WAIT
+#define PT_SLAB_WAIT 0
+#endif
+#ifndef PT_WG_NOP
+#define PT_WG_NOP 0
+#endif
 constexpr int NGRP = 16;
 constexpr int BNB_WG_PER_CLIP = 8;     // backward producers per clip at most (PW_PARTS)
 __host__ __device__ inline int bn_gsize(int nprod) { return (nprod + NGRP - 1) / NGRP; }
@@ -275,10 +284,17 @@ __device__ void stage_x(const void* __restrict__ xv, int xu8, f32x4* xs, int v, 
                        (size_t)L.tx * IMG * 3;
     for (int p = tid; p < nrows * IMG; p += nthreads) {
       const uint8_t* q = x + ((size_t)(p >> 5) * W + (p & 31)) * 3;
+      // the 3 bytes from aligned dwords (no sub-dword global loads, see ld_bf16_bits)
+      const uintptr_t qa = (uintptr_t)q;
+      const uint32_t* qw = (const uint32_t*)(qa & ~(uintptr_t)3);
+      const int sh = (int)(qa & 3) * 8;
+      uint64_t w = qw[0];
+      if (sh >= 16) w |= (uint64_t)qw[1] << 32;
+      w >>= sh;
       f32x4 v4;
-      v4[0] = (float)((double)q[0] / 255.0);
-      v4[1] = (float)((double)q[1] / 255.0);
-      v4[2] = (float)((double)q[2] / 255.0);
+      v4[0] = (float)((double)(uint32_t)(w & 0xff) / 255.0);
+      v4[1] = (float)((double)(uint32_t)((w >> 8) & 0xff) / 255.0);
+      v4[2] = (float)((double)(uint32_t)((w >> 16) & 0xff) / 255.0);
       v4[3] = 0.f;
       xs[p] = v4;
     }
@@ -843,6 +859,11 @@ template <class S, class V>
 __device__ __forceinline__ void gacc_row(float* gacc_g, float* flush, const f32x16& d,
                                          const V& x, int lane, int wave, int tid) {
   const f32x16 t = wgrad_cl<S>(d, x, zero16());
+#if PT_WG_NOP
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
   const int ci = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int r = 0; r < 16; ++r) flush[wave * SCR_FLOATS + cl_x(r, h) * 32 + ci] = t[r];
@@ -867,10 +888,18 @@ __device__ __forceinline__ void slab_range(const float* slab_p, float* slabl, in
                                            int wave, int lane) {
   const int nchunk = nf / 4;                             // 16-B chunks
   for (int j = wave; j * 64 < nchunk; j += PW_NW)
-    if (j * 64 + lane < nchunk)
+    if (j * 64 + lane < nchunk) {
+#if PT_SLAB_DMA
       __builtin_amdgcn_global_load_lds((const void*)(slab_p + f0 + (j * 64 + lane) * 4),
                                        (__attribute__((address_space(3))) void*)(slabl + f0 + j * 256),
                                        16, 0, 0);
+#else
+      *(f32x4*)(slabl + f0 + (j * 64 + lane) * 4) = *(const f32x4*)(slab_p + f0 + (j * 64 + lane) * 4);
+#endif
+    }
+#if PT_SLAB_WAIT
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 __device__ __forceinline__ void slab_prefetch(const float* slab_p, float* slabl, int g0, int ng,
                                               int wave, int lane) {
@@ -2128,7 +2157,7 @@ __global__ void k_to_nchw(const S* __restrict__ src, float* __restrict__ dst, in
   const int n = B * NPIX * C;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int c = e % C, pix = (e / C) % NPIX, v = e / (C * NPIX);
-    if (c < Cu) dst[nchw_off(v, pix, c, T, t, ntx, nty, Cu)] = ldf(src + e);
+    if (c < Cu) dst[nchw_off(v, pix, c, T, t, ntx, nty, Cu)] = ldg(src + e);
   }
 }
 __global__ void k_from_nchw(const float* __restrict__ src, float* __restrict__ dst, int B, int ntx,
@@ -2509,12 +2538,9 @@ inline bool syncbn(const pt_cell_dist* dist) { return dist && dist->bn_world > 1
 // The fused forward (k_fused_fa / k_fused_fb) covers the bf16 InT / hGRU cell
 // on single-tile (32x32) frames with k <= 7 and the inhibition branch; other
 // configurations, and PT_CELL_FUSED=0, run the split kernels.
-bool fused_env() {
-  static const bool on = [] {
-    const char* e = getenv("PT_CELL_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+bool fused_env() {             // read per call: tests A/B the two paths in one process
+  const char* e = getenv("PT_CELL_FUSED");
+  return !(e && e[0] == '0');
 }
 bool use_fused(const pt_cell_desc* d, const Plan& p) {
   return fused_env() && d->dtype == PT_DTYPE_BF16 && p.ntx * p.nty == 1 &&
@@ -2670,9 +2696,16 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
     c.bnb = sync ? dist->bn_buf + sync_b + ((size_t)t * 2 + bn) * 64 : bnb_slot(a, t, bn, nprod).grp;
     c.bnb_ngrp = sync ? 1 : bn_ngrp(nprod);
   };
+  // diagnostics only (env PT_CELL_DEBUG_STOP = n): return after the sweep's
+  // first n launches, leaving the transients as that launch wrote them
+  const char* dbg = getenv("PT_CELL_DEBUG_STOP");
+  const int stop_at = dbg ? atoi(dbg) : 0;
+  int n_launch = 0;
+  auto stop = [&] { return stop_at > 0 && ++n_launch >= stop_at; };
   a.t = p.T - 1;
   a.conv_done = 0;
   timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+  if (stop()) return 0;
   if (int rc = sync_bwd(p.T - 1, 1, p.B * PWA_WGPC)) return rc;
   for (int t = p.T - 1; t >= 0; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
@@ -2683,8 +2716,10 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
     cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
     timed(PT_K_CONV_BB, st, [&] {
       launch_conv_bwd<S>(p, st, cb); });
+    if (stop()) return 0;
     a.t = t;
     timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
+    if (stop()) return 0;
     a.conv_done = 0;
     if (!d->no_inh) {
       if (int rc = sync_bwd(t, 0, p.B * PWB_WGPC)) return rc;
@@ -2702,9 +2737,11 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
         timed(PT_K_CONV_BA, st, [&] {
           hipLaunchKernelGGL((k_bnbwd_fill<S>), dim3(p.B), dim3(NT), lcv, st, ca); });
       }
+      if (stop()) return 0;
     }
     a.t = t - 1;
     timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+    if (stop()) return 0;
     if (t >= 1)
       if (int rc = sync_bwd(t - 1, 1, p.B * PWA_WGPC)) return rc;
   }
@@ -2719,7 +2756,8 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
 // off while kernel timing is enabled (that pass wants per-launch events).
 ptg::GraphCache g_graphs;
 bool use_graph() {
-  return ptg::graphs_enabled() && __atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) == 0;
+  return ptg::graphs_enabled() && __atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) == 0 &&
+         !getenv("PT_CELL_DEBUG_STOP");
 }
 int ablate_env() {
   const char* ab = getenv("PT_CELL_ABLATE");
@@ -2760,7 +2798,8 @@ int pt_cell_forward_dist(const pt_cell_desc* d, const void* x, const pt_cell_par
   if (!use_graph() || syncbn(dist)) return body(st);
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
-  k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env());
+  k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env())
+      .add(fused_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 

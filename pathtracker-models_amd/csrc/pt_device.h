@@ -85,10 +85,43 @@ __device__ __forceinline__ float ldf(const bf16_t* p) { return (float)*p; }
 __device__ __forceinline__ void stf(float* p, float v) { *p = v; }
 __device__ __forceinline__ void stf(bf16_t* p, float v) { *p = (bf16_t)v; }
 
+// bf16 from global memory by 4-B loads of the channel pair, the lane's half
+// picked by one v_perm_b32 (PT_LD32, default): the 2-B loads
+// (global_load_ushort) returned zeros in one 16-lane quarter of a load now and
+// then on some boxes (tools/det_locate.py: dcE = 0 at one pixel, channels
+// 16-31), which the dword loads of the f32 path never did.  Same instruction
+// count; the perm replaces the shift that widened the 2-B load.
+#ifndef PT_LD32
+#define PT_LD32 1
+#endif
+__device__ __forceinline__ uint32_t bf16_sel(int c) { return (c & 1) ? 0x03020c0cu : 0x01000c0cu; }
+__device__ __forceinline__ float ldg(const float* p) { return *p; }
+__device__ __forceinline__ float ldg(const bf16_t* p) {
+#if PT_LD32
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t w = *(const uint32_t*)(a & ~(uintptr_t)3);
+  return __uint_as_float((a & 2) ? (w & 0xffff0000u) : (w << 16));
+#else
+  return (float)*p;
+#endif
+}
+
 // Load / store one CL row tile from a channels-last [32 px][32 ch] row.
 template <class S>
 __device__ __forceinline__ f32x16 load_cl(const S* __restrict__ row, int c, int h) {
   f32x16 v;
+#if PT_LD32
+  if constexpr (sizeof(S) == 2) {
+    const uint32_t* w = (const uint32_t*)(row + (c & ~1));      // 64-B aligned rows
+    const uint32_t sel = bf16_sel(c);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t x = w[cl_x(r, h) * (C / 2)];
+      v[r] = __uint_as_float(__builtin_amdgcn_perm(x, x, sel));
+    }
+    return v;
+  }
+#endif
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = ldf(row + cl_x(r, h) * C + c);
   return v;
@@ -109,6 +142,21 @@ template <class S> using Pk = typename PkT<S>::type;
 template <class S>
 __device__ __forceinline__ Pk<S> load_pk(const S* __restrict__ row, int c, int h) {
   Pk<S> v;
+#if PT_LD32
+  if constexpr (sizeof(S) == 2) {
+    const uint32_t* w = (const uint32_t*)(row + (c & ~1));
+    // elements r (low half) and r + 1 (high half) of one packed register
+    const uint32_t sel = (c & 1) ? 0x07060302u : 0x05040100u;
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    u32x8 pk;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t lo = w[cl_x(2 * k, h) * (C / 2)], hi = w[cl_x(2 * k + 1, h) * (C / 2)];
+      pk[k] = __builtin_amdgcn_perm(hi, lo, sel);
+    }
+    return __builtin_bit_cast(Pk<S>, pk);
+  }
+#endif
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = row[cl_x(r, h) * C + c];
   return v;

@@ -524,9 +524,9 @@ __global__ void k_lcolsum(const S* __restrict__ src, float* __restrict__ part, i
   int r = blockIdx.x * 2 + r0;
   for (; r + 7 * step < npix; r += 8 * step) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += ldf(src + (size_t)(r + j * step) * GC + c);
+    for (int j = 0; j < 8; ++j) s[j] += ldg(src + (size_t)(r + j * step) * GC + c);
   }
-  for (; r < npix; r += step) s[0] += ldf(src + (size_t)r * GC + c);
+  for (; r < npix; r += step) s[0] += ldg(src + (size_t)r * GC + c);
   float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __shared__ float red[256];
   red[threadIdx.x] = t;
@@ -610,7 +610,7 @@ __global__ void k_from_cl_seq(const S* __restrict__ src, float* __restrict__ dst
     const int pix = (int)(e % NPIX), t = (int)((e / NPIX) % T);
     const size_t bc = e / ((size_t)NPIX * T);
     const int c = (int)(bc % nc), b = (int)(bc / nc);
-    dst[e] = ldf(src + (((size_t)t * B + b) * NPIX + pix) * HC + c);
+    dst[e] = ldg(src + (((size_t)t * B + b) * NPIX + pix) * HC + c);
   }
 }
 template <class S>
@@ -619,7 +619,7 @@ __global__ void k_from_cl(const S* __restrict__ src, float* __restrict__ dst, in
   const int n = B * nc * NPIX;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int pix = e % NPIX, c = (e / NPIX) % nc, b = e / (NPIX * nc);
-    dst[(((size_t)b * nc + c) * tn + t) * NPIX + pix] = ldf(src + ((size_t)b * NPIX + pix) * HC + c);
+    dst[(((size_t)b * nc + c) * tn + t) * NPIX + pix] = ldg(src + ((size_t)b * NPIX + pix) * HC + c);
   }
 }
 
