@@ -164,7 +164,8 @@ enum { PT_K_PW_FA = 0, PT_K_CONV_FA = 1, PT_K_PW_FB = 2, PT_K_CONV_FB = 3,
        PT_K_PW_BA = 4, PT_K_CONV_BA = 5, PT_K_PW_BB = 6, PT_K_CONV_BB = 7,
        PT_K_WGRAD = 8, PT_K_PREP = 9, PT_K_REDUCE = 10,
        PT_K_FUSED_FA = 11, PT_K_FUSED_FB = 12,     /* bf16 32x32: point-wise + conv per launch */
-       PT_K_NKINDS = 13 };
+       PT_K_PERSIST = 13,                          /* opt-in persistent forward, all frames */
+       PT_K_NKINDS = 14 };
 int pt_cell_timing_enable(uint32_t kind_mask);      /* bit k enables kind k; 0 disables */
 int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches);
 int pt_cell_timing_reset(void);

@@ -79,6 +79,8 @@ struct BnSlot {       // one (frame, BatchNorm) reduction
   double* grp;        // [NGRP][NV] group sums (NV: 96 forward, 64 backward)
   unsigned* cnt;      // [NGRP] arrival tickets, zeroed before every call
   int nprod;          // producers in the launch
+  unsigned* done;     // persistent forward: groups summed so far (the grid wait's
+                      // counter); the group sums then go out write-through
 };
 
 __device__ __forceinline__ float ld_sc1(const float* p) {
@@ -96,8 +98,33 @@ __device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
   const int G = bn_gsize(s.nprod), m0 = g * G, m1 = min(s.nprod, m0 + G);
   const int v = tid & 63, q = tid >> 6;
   double a = 0.0, b = 0.0;
+  // every load of this thread in flight at once (the tail of the launch waits
+  // on this one workgroup), then added in member order
+  // G / Q at B = 256: k_pw_bb 128 / 4, k_pw_ba 32 / 4, the convs 16 / 8
+#ifndef PT_GS_PER
+#define PT_GS_PER 0       // 32 (all loads in flight): k_pw_bb 69.7 -> 78.8 us; 8: 70.2
+#endif
+  constexpr int MAXPER = Q <= 4 ? PT_GS_PER : (PT_GS_PER < 4 ? PT_GS_PER : 4);
+  float xv[MAXPER > 0 ? MAXPER : 1];
+#pragma unroll
+  for (int k = 0; k < MAXPER; ++k) {
+    const int m = m0 + q + k * Q;
+    xv[k] = 0.f;
+    if (m < m1) {
+      const float* pp = s.part + (size_t)m * 64 + v;
+      xv[k] = PT_BN_MODE == 2 ? ld_sc1(pp) : *pp;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXPER; ++k) {
+    if (m0 + q + k * Q < m1) {
+      const double x = (double)xv[k];
+      a += x;
+      b += x * x;
+    }
+  }
 #pragma unroll 8
-  for (int m = m0 + q; m < m1; m += Q) {
+  for (int m = m0 + q + MAXPER * Q; m < m1; m += Q) {   // larger groups than planned for
     const float* pp = s.part + (size_t)m * 64 + v;
     const double x = (double)(PT_BN_MODE == 2 ? ld_sc1(pp) : *pp);
     a += x;
@@ -114,12 +141,40 @@ __device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
       sa += scr[W * (k * 64 + tid)];
       if (FWD) sb += scr[W * (k * 64 + tid) + 1];
     }
+    double* o = s.grp + (size_t)g * (FWD ? 96 : 64);
+    auto put = [&](int i, double v) {
+      if (s.done) __hip_atomic_store(o + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else o[i] = v;
+    };
     if (FWD) {
-      double* o = s.grp + (size_t)g * 96;
-      if (tid < 32) { o[tid] = sa; o[32 + tid] = sb; }
-      else o[32 + tid] = sa;                           // sum M2_b at 64 + (tid - 32)
+      if (tid < 32) { put(tid, sa); put(32 + tid, sb); }
+      else put(32 + tid, sa);                          // sum M2_b at 64 + (tid - 32)
     } else {
-      s.grp[(size_t)g * 64 + tid] = sa;
+      put(tid, sa);
+    }
+    if (s.done) {                   // the group sum is in L2: count it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) __hip_atomic_fetch_add(s.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Persistent forward: the calling WAVE waits until `target` group sums of a
+// reduction are in (its BnSlot::done counter); no workgroup barrier (the
+// caller's next one publishes what the wave then computes).  Lane 0 polls with
+// coherent loads; the spin is bounded (a grid that is not fully resident
+// would otherwise never return): past the bound it gives up and flags *err,
+// the results are then garbage.
+__device__ __forceinline__ void wave_wait(const unsigned* done, unsigned target, unsigned* err, int lane) {
+  if (lane == 0) {
+    unsigned it = 0;
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++it & 1023) == 0 &&       // ~0.1 s, or another workgroup already gave up
+          (it > (1u << 21) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
     }
   }
 }
@@ -387,13 +442,17 @@ __device__ __forceinline__ void stem_cl(const f32x4* xs, int yl, int h, const St
 // (sum mean_b)^2 / B)); all threads end with them in stat[0..63].
 // Lanes fl < 32 of ONE wave finalise (the caller picks the wave; others pass
 // fl >= 32); stat is read only after the caller's next workgroup barrier.
+template <bool COH = false>           // COH: the sums were written in this launch (persistent)
 __device__ void bn_fwd_finalize(const double* __restrict__ grp, int ng, int B, float eps,
                                 float* stat, float* gstat, int fl) {
   if (fl < 32) {
     const int tid = fl;
     double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    auto ld = [&](int i) {
+      return COH ? __hip_atomic_load(grp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : grp[i];
+    };
     for (int k = 0; k < ng; ++k) {
-      s1 += grp[k * 96 + tid]; s2 += grp[k * 96 + 32 + tid]; s3 += grp[k * 96 + 64 + tid];
+      s1 += ld(k * 96 + tid); s2 += ld(k * 96 + 32 + tid); s3 += ld(k * 96 + 64 + tid);
     }
     const double mean = s1 / B;
     double m2 = s3 + (double)NPIX * (s2 - s1 * s1 / B);
@@ -740,7 +799,10 @@ constexpr int PWF_RPP = 1;                         // forward rows per wave
 // k_pw_bb stays at one row per wave: looping its body spills (~46 VGPRs) and
 // doubled its row cost.
 constexpr int PWA_RPP = 4;                         // k_pw_ba rows per wave
-constexpr int PWB_RPP = 1;                         // k_pw_bb rows per wave (register bound)
+#ifndef PT_PWB_RPP
+#define PT_PWB_RPP 1
+#endif
+constexpr int PWB_RPP = PT_PWB_RPP;                // k_pw_bb rows per wave (register bound)
 constexpr int PWF_WGPC = IMG / (PW_NW * PWF_RPP);  // workgroups per clip (8)
 constexpr int PWA_WGPC = IMG / (PW_NW * PWA_RPP);  // (2)
 constexpr int PWB_WGPC = IMG / (PW_NW * PWB_RPP);  // (8)
@@ -965,9 +1027,8 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, const BnSlot& out
 // -------------------------------------------------------------------------
 template <class S> struct FaIn { Pk<S> Iv, egv, cev; f32x16 Eo; };
 template <class S>
-__device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, size_t ro, int c, int h) {
+__device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
   const size_t fs = fr_off(1, a.B);
-  const int t = a.t;
   FaIn<S> w;
   w.Iv = zero_pk<S>(); w.Eo = zero16(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
   if (t > 0) {
@@ -990,12 +1051,12 @@ __device__ __forceinline__ void tile_put_cl(S* tile, int y, int c, int h, const 
 }
 
 template <class S, int ACT, int HG>
-__device__ __forceinline__ void fa_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
+__device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float* stat, const f32x4* xs,
                                        int yl, float* wscr, int b, int y, size_t ro,
                                        const FaIn<S>& in, int lane, S* tile = nullptr) {
   using F = typename Tr<S>::frag;
   const int c = lane & 31, h = lane >> 5;
-  const int t = a.t, T = a.T;
+  const int T = a.T;
   const size_t fs = fr_off(1, a.B);
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   const float kap = a.kappa[c], gam = a.gamma[c], bw1 = a.bnw1[c], bb1 = a.bnb1[c];
@@ -1085,11 +1146,11 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   if (finw && t > 0 && !(a.ablate & 65536))
     bn_fwd_finalize(bnf_src(a, t - 1, 1), bnf_nsrc(a), B * a.bn_world, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
-  const FaIn<S> in = fa_load(a, ro, c, h);
+  const FaIn<S> in = fa_load(a, t, ro, c, h);
   if (t < T && !(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   __syncthreads();
   if (a.ablate & 4) return;
-  fa_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, b, y, ro, in, lane);
+  fa_row<S, ACT, HG>(a, t, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, b, y, ro, in, lane);
 }
 
 // -------------------------------------------------------------------------
@@ -1099,9 +1160,8 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
 // -------------------------------------------------------------------------
 template <class S> struct FbIn { Pk<S> civ, Iv, gi; };
 template <class S, int HG>
-__device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, size_t ro, int c, int h) {
+__device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
   const size_t fs = fr_off(1, a.B);
-  const int t = a.t;
   FbIn<S> w;
   w.civ = load_pk(a.ci + t * fs + ro, c, h);
   w.Iv = t > 0 ? load_pk(a.I + (t - 1) * fs + ro, c, h) : zero_pk<S>();
@@ -1112,7 +1172,7 @@ __device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, size_t ro, int 
 
 // One image row of forward point-wise B (BN0 stats of frame t in stat[0..63]).
 template <class S, int ACT, int HG>
-__device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, const f32x4* xs,
+__device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float* stat, const f32x4* xs,
                                        int yl, float* wscr, int y, size_t ro, const FbIn<S>& in,
                                        int lane, S* tile = nullptr) {
   using F = typename Tr<S>::frag;
@@ -1146,7 +1206,7 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, const float* stat, 
   if (sizeof(S) == 4 && (a.ablate & 4096))
 #pragma unroll
     for (int r = 0; r < 16; ++r) In[r] = (float)(bf16_t)In[r];
-  store_cl(a.I + a.t * fs + ro, c, h, In);
+  store_cl(a.I + t * fs + ro, c, h, In);
   if (tile) tile_put_cl(tile, y, c, h, In);
 }
 
@@ -1173,14 +1233,14 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
     }
     return;
   }
-  const FbIn<S> in = fb_load<S, HG>(a, ro, c, h);
+  const FbIn<S> in = fb_load<S, HG>(a, t, ro, c, h);
   stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   // (finalising first in a separate wave, as k_pw_fa does, measured no gain here)
   bn_fwd_finalize(bnf_src(a, t, 0), bnf_nsrc(a), B * a.bn_world, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
   if (a.ablate & 4) return;
-  fb_row<S, ACT, HG>(a, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, y, ro, in, lane);
+  fb_row<S, ACT, HG>(a, t, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, y, ro, in, lane);
 }
 
 
@@ -1216,33 +1276,40 @@ __device__ __forceinline__ FusedLds fused_carve(char* smem) {
 // The conv half: conv(tile, wf) for this wave's rows, rows stored as they
 // finish (out_raw), then the per-clip BN partials (bnout).
 template <class S>
-__device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<S>& c, char* smem,
-                                           const FusedLds& L, int b, int wave, int lane, int tid) {
+__device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<S>& c, S* out_raw,
+                                           const BnSlot& bnout, char* smem, const FusedLds& L, int b,
+                                           int wave, int lane, int tid) {
   constexpr int RW = FUSED_RW;
   f32x16 acc[RW];
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i] = zero16();
   const int h = lane >> 5, px = lane & 31;
-  const StoreRow<S> sr{c.out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h};
+  const StoreRow<S> sr{out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h};
   auto nofill = [](int) {};                 // the point-wise half filled the tile
   conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
                                    tid, 0, sr);
-  bn_fwd_partial<RW, FUSED_NW>(acc, L.red, c.bnout, b, lane, wave, tid, 0,
+  bn_fwd_partial<RW, FUSED_NW>(acc, L.red, bnout, b, lane, wave, tid, 0,
                                (int*)(smem + CONV_NT * 16), (double*)smem);
 }
 
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(CONV_NT, 1) void k_fused_fa(CellArgs<S> a, ConvArgs<S> c) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+template <class S, int ACT, int HG, bool COH>
+__device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvArgs<S>& c, int t, S* out_raw,
+                                              const BnSlot& bnout, char* smem, int tid,
+                                              const unsigned* wcnt = nullptr, unsigned wtarget = 0,
+                                              unsigned* err = nullptr) {
   const FusedLds L = fused_carve<S>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 31, h = lane >> 5;
+  const int lane = tid & 63, cl = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, t = a.t;
+  const int b = blockIdx.x;
+  if constexpr (COH) __syncthreads();      // the previous segment's LDS use is over
+  // persistent: only the finalising wave waits for the batch sums (COH); the
+  // others' row loads and the x staging below go out meanwhile
+  if (COH && wave == FUSED_NW - 1 && t > 0) wave_wait(wcnt, wtarget, err, lane);
   if (wave == FUSED_NW - 1 && t > 0)
-    bn_fwd_finalize(bnf_src(a, t - 1, 1), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat + 64,
-                    b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
+    bn_fwd_finalize<COH>(bnf_src(a, t - 1, 1), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat + 64,
+                         b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   // this wave's first row's tiles go out before the staging and the barrier
-  FaIn<S> nxt = fa_load(a, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
+  FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
   stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
@@ -1251,24 +1318,28 @@ __global__ __launch_bounds__(CONV_NT, 1) void k_fused_fa(CellArgs<S> a, ConvArgs
     const int y = wave * FUSED_RW + i;
     const size_t ro = clip_off(b) + (size_t)y * IMG * C;
     const FaIn<S> cur = nxt;
-    if (i + 1 < FUSED_RW) nxt = fa_load(a, ro + (size_t)IMG * C, cl, h);   // next row in flight
-    fa_row<S, ACT, HG>(a, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
+    if (i + 1 < FUSED_RW) nxt = fa_load(a, t, ro + (size_t)IMG * C, cl, h);   // next row in flight
+    fa_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
                        (S*)L.tile);
   }
-  fused_conv<S>(a, c, smem, L, b, wave, lane, tid);
+  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
 }
 
-template <class S, int ACT, int HG>
-__global__ __launch_bounds__(CONV_NT, 1) void k_fused_fb(CellArgs<S> a, ConvArgs<S> c) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+template <class S, int ACT, int HG, bool COH>
+__device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvArgs<S>& c, int t, S* out_raw,
+                                              const BnSlot& bnout, char* smem, int tid,
+                                              const unsigned* wcnt = nullptr, unsigned wtarget = 0,
+                                              unsigned* err = nullptr) {
   const FusedLds L = fused_carve<S>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 31, h = lane >> 5;
+  const int lane = tid & 63, cl = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, t = a.t;
+  const int b = blockIdx.x;
+  if constexpr (COH) __syncthreads();
+  if (COH && wave == FUSED_NW - 1) wave_wait(wcnt, wtarget, err, lane);
   if (wave == FUSED_NW - 1)
-    bn_fwd_finalize(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
-                    b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
-  FbIn<S> nxt = fb_load<S, HG>(a, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
+    bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
+                         b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
+  FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
   stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
@@ -1277,11 +1348,61 @@ __global__ __launch_bounds__(CONV_NT, 1) void k_fused_fb(CellArgs<S> a, ConvArgs
     const int y = wave * FUSED_RW + i;
     const size_t ro = clip_off(b) + (size_t)y * IMG * C;
     const FbIn<S> cur = nxt;
-    if (i + 1 < FUSED_RW) nxt = fb_load<S, HG>(a, ro + (size_t)IMG * C, cl, h);
-    fb_row<S, ACT, HG>(a, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
+    if (i + 1 < FUSED_RW) nxt = fb_load<S, HG>(a, t, ro + (size_t)IMG * C, cl, h);
+    fb_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
                        (S*)L.tile);
   }
-  fused_conv<S>(a, c, smem, L, b, wave, lane, tid);
+  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
+}
+
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(CONV_NT, 1) void k_fused_fa(CellArgs<S> a, ConvArgs<S> c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  fused_fa_body<S, ACT, HG, false>(a, c, a.t, c.out_raw, c.bnout, smem, threadIdx.x);
+}
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(CONV_NT, 1) void k_fused_fb(CellArgs<S> a, ConvArgs<S> c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  fused_fb_body<S, ACT, HG, false>(a, c, a.t, c.out_raw, c.bnout, smem, threadIdx.x);
+}
+
+// Persistent forward (PT_CELL_PERSIST=1): the fused segments of all T frames
+// in ONE launch of B workgroups, all resident (one per CU; the host checks
+// the occupancy).  The two BatchNorm syncs per frame become in-launch waits:
+// every workgroup publishes its partials (write-through + ticket), the last of
+// each group stores the group sum write-through and counts it in done[t][bn];
+// every workgroup's finalising wave waits for all groups (wave_wait).  Same
+// arithmetic and reduction order as the per-segment launches.
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(CONV_NT, 1) void k_persist_fwd(const CellArgs<S> a, const ConvArgs<S> ca,
+                                                            const ConvArgs<S> cb, unsigned* done,
+                                                            unsigned* err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const size_t fs = fr_off(1, a.B);
+  const unsigned ng = (unsigned)bn_ngrp(a.B);
+#pragma unroll 1
+  for (int t = 0; t < a.T; ++t) {
+    // the weight pointers and the thread index laundered per frame: hoisted
+    // out of the frame loop, the per-lane weight-fragment and LDS addresses
+    // pinned ~130 VGPRs (2 KB of spills)
+    ConvArgs<S> cx = ca;
+    asm volatile("" : "+s"(cx.wf));
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
+    BnSlot s0 = bnf_slot(a, t, 0);
+    s0.done = done + 2 * t;
+    fused_fa_body<S, ACT, HG, true>(a, cx, t, a.ci + t * fs, s0, smem, tl,
+                                    done + 2 * (t - 1) + 1, ng, err);   // waits for BN1 of t-1
+    ConvArgs<S> cy = cb;
+    asm volatile("" : "+s"(cy.wf));
+    tl = tid;
+    asm volatile("" : "+v"(tl));
+    BnSlot s1 = bnf_slot(a, t, 1);
+    s1.done = done + 2 * t + 1;
+    fused_fb_body<S, ACT, HG, true>(a, cy, t, a.ce + t * fs, s1, smem, tl,
+                                    done + 2 * t, ng, err);             // waits for BN0 of t
+  }
 }
 
 // -------------------------------------------------------------------------
@@ -2261,6 +2382,11 @@ static int fail(int code, const char* fmt, const char* a = "", long v = 0) {
   snprintf(g_err, sizeof(g_err), fmt, a, v);
   return code;
 }
+// the library's other translation units (pt_readout.hip) report through here
+__attribute__((visibility("hidden"))) int pt_set_error(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
 
 namespace {
 
@@ -2313,6 +2439,7 @@ struct Plan {
   size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], o_pad, saved;
   // workspace offsets
   size_t o_bnf_cnt, o_bnf_part, o_bnf_grp, o_bnb_cnt, o_bnb_part, o_bnb_grp;   // BnSlot storage
+  size_t o_bnf_done, o_err;   // persistent forward: group-sum counters [T][2], give-up flag
   size_t bnf_cnt_bytes, bnb_cnt_bytes;
   size_t o_tr[NTRANS], o_dci, o_dce, o_slab, o_wslab, ws;
   int nwg;
@@ -2363,6 +2490,8 @@ Plan plan(const pt_cell_desc* d) {
   // tickets first (the only words cleared per call), then partials and group sums
   // (PT_BN_MODE 0 accumulates into the group sums: they are cleared too)
   p.o_bnf_cnt = o; o += al((size_t)p.T * 2 * NGRP * 4);
+  p.o_bnf_done = o; o += al((size_t)p.T * 2 * 4);
+  p.o_err = o; o += al(4);
   p.o_bnf_grp = o; o += al((size_t)p.T * 2 * NGRP * 96 * 8);
   p.bnf_cnt_bytes = PT_BN_MODE == 0 ? o - p.o_bnf_cnt : p.o_bnf_grp - p.o_bnf_cnt;
   p.o_bnf_part = o; o += al((size_t)p.T * 2 * p.B * 64 * 4);
@@ -2492,6 +2621,10 @@ int set_lds_attrs() {
   SETLDS((k_fused_fb<S, 0, 1>), fused_lds_bytes<S>());
   SETLDS((k_fused_fb<S, 1, 0>), fused_lds_bytes<S>());
   SETLDS((k_fused_fb<S, 1, 1>), fused_lds_bytes<S>());
+  SETLDS((k_persist_fwd<S, 0, 0>), fused_lds_bytes<S>());
+  SETLDS((k_persist_fwd<S, 0, 1>), fused_lds_bytes<S>());
+  SETLDS((k_persist_fwd<S, 1, 0>), fused_lds_bytes<S>());
+  SETLDS((k_persist_fwd<S, 1, 1>), fused_lds_bytes<S>());
   SETLDS((k_wgrad<S, PADMAX>), (wgrad_lds_bytes<S, PADMAX>()));
   SETLDS((k_wgrad<S, PADBIG>), (wgrad_lds_bytes<S, PADBIG>()));
   done = true;
@@ -2547,6 +2680,29 @@ bool use_fused(const pt_cell_desc* d, const Plan& p) {
          p.K <= 2 * PADMAX + 1 && !d->no_inh;
 }
 
+// Persistent forward (k_persist_fwd): opt-in (PT_CELL_PERSIST=1, read per
+// call) on the fused configurations without SyncBN, and only when the B
+// workgroups are all resident at once (occupancy x CUs, checked per device).
+bool persist_env() {
+  const char* e = getenv("PT_CELL_PERSIST");
+  return e && e[0] == '1';
+}
+template <class S>
+bool persist_fits(int B) {
+  static int cap[2] = {-1, -1};           // per storage type; one device per process
+  int& c = cap[sizeof(S) == 2];
+  if (c < 0) {
+    int dev = 0, ncu = 0, per = 0;
+    c = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_persist_fwd<S, 0, 0>, CONV_NT,
+                                                     fused_lds_bytes<S>()) == hipSuccess)
+      c = per * ncu;
+  }
+  return B <= c;
+}
+
 int check_dist(const pt_cell_dist* dist) {
   if (!dist) return 0;
   if (dist->bn_world < 1) return fail(PT_ERR_ARG, "bn_world must be >= 1%s (got %ld)", "", dist->bn_world);
@@ -2588,7 +2744,22 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
   ca.wf = a.wf_inh;
   cb.wf = a.wf_exc;
-  if (use_fused(d, p)) {        // one launch per BatchNorm segment (k_fused_fa / k_fused_fb)
+  if (use_fused(d, p) && !syncbn(dist) && persist_env() && persist_fits<S>(p.B)) {
+    unsigned* done = (unsigned*)((char*)ws + p.o_bnf_done);
+    unsigned* err = (unsigned*)((char*)ws + p.o_err);
+    timed(PT_K_PERSIST, st, [&] {
+      const size_t lds = fused_lds_bytes<S>();
+      if (a.hgru) {
+        if (a.act) hipLaunchKernelGGL((k_persist_fwd<S, 1, 1>), dim3(p.B), dim3(CONV_NT), lds, st, a, ca, cb, done, err);
+        else hipLaunchKernelGGL((k_persist_fwd<S, 0, 1>), dim3(p.B), dim3(CONV_NT), lds, st, a, ca, cb, done, err);
+      } else {
+        if (a.act) hipLaunchKernelGGL((k_persist_fwd<S, 1, 0>), dim3(p.B), dim3(CONV_NT), lds, st, a, ca, cb, done, err);
+        else hipLaunchKernelGGL((k_persist_fwd<S, 0, 0>), dim3(p.B), dim3(CONV_NT), lds, st, a, ca, cb, done, err);
+      }
+    });
+    a.t = p.T;
+    timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });     // closes E_{T-1}
+  } else if (use_fused(d, p)) {   // one launch per BatchNorm segment (k_fused_fa / k_fused_fb)
     for (int t = 0; t < p.T; ++t) {
       a.t = t;
       ca.out_raw = a.ci + t * fs; ca.bnout = bnf_slot(a, t, 0);
@@ -2799,7 +2970,8 @@ int pt_cell_forward_dist(const pt_cell_desc* d, const void* x, const pt_cell_par
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
   k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env())
-      .add(fused_env());
+      .add(fused_env())
+      .add(persist_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 

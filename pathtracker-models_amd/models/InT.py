@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn import init
 
+from ptamd import readout as ro
 from ptamd.cell import PARAM_KEYS, CellConfig, run_cell, target_channel
 
 _DEFAULT_DTYPE = os.environ.get("PT_CELL_DTYPE", "f32")
@@ -168,11 +169,9 @@ class InT(nn.Module):
         return [sd.get(k) for k in PARAM_KEYS]
 
     def readout(self, e_last, x):
-        """models/InT.py:236-241"""
-        out = torch.cat([self.readout_conv(e_last), target_channel(x)[:, None]], 1)
-        out = self.target_conv(out)
-        out = F.avg_pool2d(out, kernel_size=out.size()[2:])
-        return self.readout_dense(out.reshape(x.shape[0], -1))
+        """models/InT.py:236-241 (fused HIP kernels on ROCm tensors: ptamd/readout.py)"""
+        return ro.readout(e_last, target_channel(x), self.readout_conv, self.target_conv,
+                          self.readout_dense)
 
     # forward also takes the raw u8 clips [B,T,H,W,3] (engine.prepare_data
     # keep_u8): the kernels convert them exactly as prepare_data would

@@ -31,6 +31,7 @@ from torch.autograd import Function
 from torch.nn import init
 
 from ptamd import lstm
+from ptamd import readout as ro
 from ptamd.cell import target_channel
 from ptamd.lstm import run_steps
 
@@ -263,10 +264,8 @@ class ConvLSTMVideo(nn.Module):
         want_jv = self.training and steps >= 2
         res = self.unit1.steps(xbn, steps, want_jv=want_jv, want_seq=testmode)
         h_t, jv = res[0], res[2]
-        out = torch.cat([self.readout_conv(h_t), target_channel(x)[:, None]], 1)
-        out = self.target_conv(out)
-        out = F.avg_pool2d(out, kernel_size=out.size()[2:])
-        out = self.readout_dense(out.reshape(x.shape[0], -1))
+        out = ro.readout(h_t, target_channel(x), self.readout_conv, self.target_conv,
+                         self.readout_dense)                         # ptamd/readout.py
         if testmode:
             hidden = res[3].permute(0, 2, 1, 3, 4)                  # [B, T, C, H, W]
             b, t, c, h, w = hidden.shape

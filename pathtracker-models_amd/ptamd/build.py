@@ -22,9 +22,9 @@ INC = os.path.join(REPO, "include")
 
 # library -> (sources, extra dependencies)
 LIBS = {
-    "libptcell.so": ([os.path.join(CSRC, "pt_cell.hip")],
+    "libptcell.so": ([os.path.join(CSRC, "pt_cell.hip"), os.path.join(CSRC, "pt_readout.hip")],
                      [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
-                      os.path.join(INC, "pt_cell.h")]),
+                      os.path.join(INC, "pt_cell.h"), os.path.join(INC, "pt_readout.h")]),
     "libpttfr.so": ([os.path.join(CSRC, "pt_tfrecord.cpp")], [os.path.join(INC, "pt_tfrecord.h")]),
     "libptlstm.so": ([os.path.join(CSRC, "pt_lstm.hip")],
                      [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),

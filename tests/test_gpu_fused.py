@@ -4,7 +4,12 @@ frames) against the split kernels (k_pw_fa, k_conv_fwd, k_pw_fb, k_conv_fwd):
 the arithmetic is the same operation for operation (the LDS tile holds the
 bf16 values the split conv would load), so logits, per-frame testmode outputs
 and every gradient must agree bit for bit.  PT_CELL_FUSED=0 selects the split
-path (read per call by the library)."""
+path (read per call by the library).
+
+The persistent forward (k_persist_fwd, PT_CELL_PERSIST=1: all T frames of the
+fused segments in one launch, the BatchNorm syncs as in-launch waits on the
+deterministic group sums) is the same arithmetic in the same reduction order,
+so it too must reproduce the per-segment launches bit for bit."""
 import os
 
 import pytest
@@ -20,8 +25,9 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _run(m, x, y, fused):
+def _run(m, x, y, fused, persist=False):
     os.environ["PT_CELL_FUSED"] = "1" if fused else "0"
+    os.environ["PT_CELL_PERSIST"] = "1" if persist else "0"
     try:
         m.zero_grad(set_to_none=True)
         out, _ = m(x)
@@ -33,11 +39,22 @@ def _run(m, x, y, fused):
                 {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None})
     finally:
         os.environ.pop("PT_CELL_FUSED", None)
+        os.environ.pop("PT_CELL_PERSIST", None)
 
 
 @pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("int", "tanh", 5, 3),
                                           ("hgru", "softplus", 16, 6), ("int", "softplus", 256, 64)])
 def test_fused_forward_is_bitwise_the_split_forward(cell, act, b, t):
+    _compare(cell, act, b, t, dict(fused=False))
+
+
+@pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("int", "tanh", 5, 3),
+                                          ("hgru", "softplus", 16, 6), ("int", "softplus", 256, 64)])
+def test_persistent_forward_is_bitwise_the_fused_forward(cell, act, b, t):
+    _compare(cell, act, b, t, dict(fused=True, persist=True))
+
+
+def _compare(cell, act, b, t, other):
     from models import InT, ffhgru_hierarchy as hg
     from ptamd import synth
     dev = _dev()
@@ -59,7 +76,7 @@ def test_fused_forward_is_bitwise_the_split_forward(cell, act, b, t):
     x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float().to(dev)
     y = torch.tensor([ord(v) for v in labels], dtype=torch.float32, device=dev)
     o1, s1, g1, gr1 = _run(m, x, y, fused=True)
-    o0, s0, g0, gr0 = _run(m, x, y, fused=False)
+    o0, s0, g0, gr0 = _run(m, x, y, **other)
     assert torch.isfinite(o1).all()
     assert torch.equal(o1, o0) and torch.equal(s1, s0) and torch.equal(g1, g0)
     for k in gr0:

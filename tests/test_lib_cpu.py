@@ -25,8 +25,9 @@ def _header_symbols(header="pt_cell.h"):
 
 
 def _bindings():
-    from ptamd import _lib, lstm, tfrecord
+    from ptamd import _lib, lstm, readout, tfrecord
     return [("pt_cell.h", _lib, "pt_version", "pt_cell"),
+            ("pt_readout.h", readout, None, None),
             ("pt_lstm.h", lstm, "pt_lstm_version", "pt_lstm"),
             ("pt_tfrecord.h", tfrecord, None, None)]
 

@@ -32,7 +32,7 @@ def main():
     kinds = [k for k in _lib.KIND_NAMES if k not in ("k_prep", "k_reduce")]
     res = {mk: {k: [] for k in kinds} for mk in masks}
     tot = {mk: {"fwd": [], "bwd": [], "all": []} for mk in masks}     # summed device ms per step
-    fwd_kinds = {"k_pw_fa", "k_conv_fa", "k_pw_fb", "k_conv_fb", "k_fused_fa", "k_fused_fb"}
+    fwd_kinds = {"k_pw_fa", "k_conv_fa", "k_pw_fb", "k_conv_fb", "k_fused_fa", "k_fused_fb", "k_persist_fwd"}
     for r in range(rounds + 1):
         for mk in masks:
             bits, _, env = mk.partition(":")
