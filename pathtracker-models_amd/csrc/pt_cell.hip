@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -2208,6 +2209,17 @@ __device__ __forceinline__ float strided_sum(const float* __restrict__ p, size_t
   return acc[0];
 }
 
+// k_reduce part 0 in two levels: the B * PW_PARTS slab partitions summed in
+// RED_NG contiguous groups (fixed order), then the group sums (k_reduce on
+// the RED_NG rows).  One level had 26 workgroups each walking 2048
+// partitions: ~100 us, latency-bound.
+constexpr int RED_NG = 32;
+__global__ void k_slab_partial(const float* __restrict__ slab, float* __restrict__ tmp, int rows) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
+  if (e >= SLAB) return;
+  const int r0 = (int)((long)g * rows / RED_NG), r1 = (int)((long)(g + 1) * rows / RED_NG);
+  tmp[(size_t)g * SLAB + e] = strided_sum(slab + (size_t)r0 * SLAB + e, SLAB, r1 - r0);
+}
 __global__ void k_reduce(ReduceArgs r) {
   const int KK = r.K * r.K;
   const int n_small = SLAB;                  // slab entries
@@ -2271,23 +2283,34 @@ __device__ __forceinline__ size_t nchw_off(int v, int pix, int c, int T, int t, 
   return (((size_t)L.b * T + t) * Cu + c) * ((size_t)nty * IMG * W) +
          (size_t)(L.ty * IMG + (pix >> 5)) * W + L.tx * IMG + (pix & 31);
 }
+// CL rows <-> NCHW: one workgroup per (tile, image row), the 32 px x 32 ch
+// row transposed through LDS so both sides are read / written contiguously.
+// grid = tiles * IMG, 256 threads.
 template <class S>
-__global__ void k_to_nchw(const S* __restrict__ src, float* __restrict__ dst, int B, int T, int t,
-                          int ntx, int nty, int Cu) {
+__global__ __launch_bounds__(256) void k_to_nchw(const S* __restrict__ src, float* __restrict__ dst, int B,
+                                                 int T, int t, int ntx, int nty, int Cu) {
   // dst [clips][T][Cu][H][W] (T=1,t=0 for a single frame); B = tiles
-  const int n = B * NPIX * C;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const int c = e % C, pix = (e / C) % NPIX, v = e / (C * NPIX);
-    if (c < Cu) dst[nchw_off(v, pix, c, T, t, ntx, nty, Cu)] = ldg(src + e);
+  __shared__ float tl[IMG][C + 1];
+  const int v = blockIdx.x / IMG, y = blockIdx.x % IMG;
+  const S* row = src + ((size_t)v * NPIX + (size_t)y * IMG) * C;
+  for (int i = threadIdx.x; i < IMG * C; i += 256) tl[i / C][i % C] = ldg(row + i);
+  __syncthreads();
+  for (int i = threadIdx.x; i < IMG * C; i += 256) {
+    const int c = i / IMG, px = i % IMG;
+    if (c < Cu) dst[nchw_off(v, y * IMG + px, c, T, t, ntx, nty, Cu)] = tl[px][c];
   }
 }
-__global__ void k_from_nchw(const float* __restrict__ src, float* __restrict__ dst, int B, int ntx,
-                            int nty, int Cu) {
-  const int n = B * NPIX * C;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const int c = e % C, pix = (e / C) % NPIX, v = e / (C * NPIX);
-    dst[e] = c < Cu ? src[nchw_off(v, pix, c, 1, 0, ntx, nty, Cu)] : 0.f;
+__global__ __launch_bounds__(256) void k_from_nchw(const float* __restrict__ src, float* __restrict__ dst,
+                                                   int B, int ntx, int nty, int Cu) {
+  __shared__ float tl[IMG][C + 1];
+  const int v = blockIdx.x / IMG, y = blockIdx.x % IMG;
+  for (int i = threadIdx.x; i < IMG * C; i += 256) {
+    const int c = i / IMG, px = i % IMG;
+    tl[px][c] = c < Cu ? src[nchw_off(v, y * IMG + px, c, 1, 0, ntx, nty, Cu)] : 0.f;
   }
+  __syncthreads();
+  float* row = dst + ((size_t)v * NPIX + (size_t)y * IMG) * C;
+  for (int i = threadIdx.x; i < IMG * C; i += 256) row[i] = tl[i / C][i % C];
 }
 
 // Channel padding (Cu < 32): the caller's parameters copied into 32-channel
@@ -2504,7 +2527,8 @@ Plan plan(const pt_cell_desc* d) {
   p.o_dce = o; o += fbytes;
   p.o_slab = o; o += al((size_t)p.B * PW_PARTS * SLAB * 4);
   p.nwg = p.B * p.T < 256 ? p.B * p.T : 256;
-  p.o_wslab = o; o += al((size_t)2 * p.nwg * p.K * p.K * 1024 * 4);
+  p.o_wslab = o;              // also k_reduce's group sums (k_slab_partial) before k_wgrad
+  o += al(std::max((size_t)2 * p.nwg * p.K * p.K * 1024 * 4, (size_t)RED_NG * SLAB * 4));
   p.ws = o;
   return p;
 }
@@ -2793,7 +2817,7 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
       if (int rc = bn_sync(dist, cb.bnout.grp, bn_ngrp(p.B), 96, ((size_t)t * 2 + 1) * 96, st)) return rc;
   }
   if (e_last)
-    hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_to_nchw<float>, dim3(p.B * IMG), dim3(256), 0, st,
                        (const float*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0, p.ntx, p.nty,
                        p.Cu);
   HIPCHK(hipGetLastError());
@@ -2849,7 +2873,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   }
   HIPCHK(zero_async((char*)ws + p.o_slab, (size_t)p.B * PW_PARTS * SLAB * 4, st));
   HIPCHK(zero_async((char*)ws + p.o_bnb_cnt, p.bnb_cnt_bytes, st));     // BN tickets
-  hipLaunchKernelGGL(k_from_nchw, dim3(256), dim3(256), 0, st, d_e_last,
+  hipLaunchKernelGGL(k_from_nchw, dim3(p.B * IMG), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty, p.Cu);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
   const size_t lpa = (pw_lds_bytes<PWA_RPP, true>()), lpb = pwb_lds_bytes<S>();
@@ -2918,7 +2942,13 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   }
   r.part = 0;
   timed(PT_K_REDUCE, st, [&] {
-    hipLaunchKernelGGL(k_reduce, dim3((SLAB + 255) / 256), dim3(256), 0, st, r); });
+    float* tmp = (float*)((char*)ws + p.o_wslab);      // free until k_wgrad (phase 1)
+    hipLaunchKernelGGL(k_slab_partial, dim3((SLAB + 255) / 256, RED_NG), dim3(256), 0, st, r.slab,
+                       tmp, r.B);
+    ReduceArgs r2 = r;
+    r2.slab = tmp;
+    r2.B = RED_NG;
+    hipLaunchKernelGGL(k_reduce, dim3((SLAB + 255) / 256), dim3(256), 0, st, r2); });
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -2985,7 +3015,7 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, p
   if (!saved || !e_seq) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
   const Plan p = plan(d);
   for (int t = 0; t < p.T; ++t) {
-    hipLaunchKernelGGL(k_to_nchw<float>, dim3(256), dim3(256), 0, (hipStream_t)stream,   // E is f32
+    hipLaunchKernelGGL(k_to_nchw<float>, dim3(p.B * IMG), dim3(256), 0, (hipStream_t)stream,   // E is f32
                        (const float*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B,
                        p.T, t, p.ntx, p.nty, p.Cu);
   }
