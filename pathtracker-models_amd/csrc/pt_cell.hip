@@ -777,6 +777,108 @@ __global__ __launch_bounds__(NTH, 1) void k_conv_bwd(ConvArgs<S> a) {     // BN 
 // waves x 8 rows: conv_fwd 34.0 -> 33.4 us, conv_bwd of the BN1 side 42.2 ->
 // 39.1 us at B=256 bf16); k > 7: 4 waves x 8 rows (the 46 x 46 tile)
 constexpr int CONV_NT = 512;
+
+// -------------------------------------------------------------------------
+// Banded backward conv (bf16, 32x32 frames, k <= 7; PT_CONV_BAND=1): TWO
+// workgroups per clip, each a 16-row band of the output (4 waves x 4 rows)
+// over a 22 x 38 halo tile (55 KB of LDS, so two workgroups share a CU and one
+// fills / finishes while the other's MFMAs run -- the whole-clip form is one
+// workgroup per CU with its fill, slice ring and epilogue serial).  B
+// fragments come from L2 into registers one column ahead (no slice ring, no
+// per-column barrier); each finished output row adds its addends and is
+// stored at once (no prefetch: the co-resident workgroup covers the latency).
+// Per output row the MFMA order is that of k_conv_bwd: results bit-identical.
+// -------------------------------------------------------------------------
+constexpr int BAND_ROWS = 16, BAND_NT = 256, BAND_TR = BAND_ROWS + 2 * PADMAX;
+constexpr int band_tile_bytes() { return BAND_TR * TILE * C * 2; }
+
+struct AddRowBand {
+  bf16_t* out;
+  const bf16_t *add0, *add1;
+  size_t po;
+  int h;
+  static constexpr bool active = true;
+  static constexpr bool prefetch_active = false;
+  static constexpr bool wreg = true;
+  __device__ __forceinline__ void prefetch() const {}
+  __device__ __forceinline__ void operator()(int i, const f32x16& acc) const {
+    f32x16 v = acc;
+    add_pl(add0 + po + (size_t)i * IMG * C, h, v);
+    if (add1) add_pl(add1 + po + (size_t)i * IMG * C, h, v);
+    store_pl(out + po + (size_t)i * IMG * C, h, v);
+  }
+};
+
+__global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a) {
+  using S = bf16_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = BAND_NT / 64, RW = BAND_ROWS / NW;
+  S* tile = (S*)smem;
+  float* tbl = (float*)(smem + band_tile_bytes());
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, px = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x >> 1, y0 = (blockIdx.x & 1) * BAND_ROWS;
+  const size_t cb = clip_off(b);
+  if (tid < 32) {     // BN backward as an affine map per channel (as conv_body)
+    const double inv = 1.0 / ((double)a.bnB * NPIX);
+    double sd = 0.0, sdx = 0.0;
+    for (int k = 0; k < a.bnb_ngrp; ++k) { sd += a.bnb[k * 64 + tid]; sdx += a.bnb[k * 64 + 32 + tid]; }
+    const float md = (float)(sd * inv), mdx = (float)(sdx * inv);
+    const float mean = a.bnstat[tid], rstd = a.bnstat[32 + tid];
+    const float A = rstd * a.bnw[tid];
+    tbl[tid] = A;
+    tbl[32 + tid] = -A * mdx * rstd;
+    tbl[64 + tid] = -A * md + A * mdx * rstd * mean;
+  }
+  {
+    uint4* z = (uint4*)tile;
+    for (int i = tid; i < band_tile_bytes() / 16; i += BAND_NT) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  // image rows of the band's tile: [y0 - PAD, y0 + 16 + PAD) within the image
+  const int r0 = y0 - PADMAX < 0 ? 0 : y0 - PADMAX;
+  const int r1 = y0 + BAND_ROWS + PADMAX > IMG ? IMG : y0 + BAND_ROWS + PADMAX;
+  auto fill = [&](int) {
+    constexpr int CPB = 8, NCH = C / CPB;
+    const int n = (r1 - r0) * IMG * NCH;
+    constexpr int BATCH = 4;
+    for (int i0 = tid; i0 < n; i0 += BATCH * BAND_NT) {
+      uint4 dv[BATCH], rv[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int idx = i0 + k * BAND_NT < n ? i0 + k * BAND_NT : i0;
+        const int pix = r0 * IMG + idx / NCH, q = idx % NCH;
+        const size_t e = cb + (size_t)pix * C + q * CPB;
+        dv[k] = *(const uint4*)(a.dc + e);
+        rv[k] = *(const uint4*)(a.raw + e);
+      }
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int idx = i0 + k * BAND_NT;
+        if (idx >= n) break;
+        const int pix = r0 * IMG + idx / NCH, q = idx % NCH, ch0 = q * CPB;
+        const S* rr = (const S*)&rv[k];
+        const S* dd = (const S*)&dv[k];
+        uint4 ov;
+        S* oo = (S*)&ov;
+#pragma unroll
+        for (int j = 0; j < CPB; ++j) {
+          const int ch = ch0 + j;
+          oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
+        }
+        const int y = pix >> 5, x = pix & 31;
+        if (y >= y0 && y < y0 + BAND_ROWS)          // each pixel written out by one band
+          *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
+        *(uint4*)(tile + tile_off<S, PADMAX>(y - y0 + PADMAX, x + PADMAX, ch0)) = ov;
+      }
+    }
+  };
+  f32x16 acc[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) acc[i] = zero16();
+  const AddRowBand ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
+                      cb + ((size_t)(y0 + wave * RW) * IMG + px) * C, h};
+  conv_run<S, PADMAX, RW, BAND_NT>(acc, fill, a.wf, tile, nullptr, a.K, wave * RW, lane, tid, a.ablate, ar);
+}
 template <class S>
 __global__ __launch_bounds__(NT, 1) void k_bnbwd_fill(ConvArgs<S> a) {   // frame 0: BN bwd only
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2663,8 +2765,23 @@ void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   else
     hipLaunchKernelGGL((k_conv_fwd<S, PADBIG>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADBIG>()), st, c);
 }
+// PT_CONV_BAND (read per call): 0 never, 1 always, unset: the one-addend
+// launches only (k_conv_ba: 38.9 -> 37.3 us; with two addends the unprefetched
+// epilogue lost: k_conv_bb 41.9 -> 42.8 us; profiles/r03_ablate_band.txt)
+int band_env() {
+  const char* e = getenv("PT_CONV_BAND");
+  return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 1 : 2;
+}
 template <class S>
 void launch_conv_bwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
+  if constexpr (sizeof(S) == 2) {
+    const int bm = band_env();
+    if ((bm == 1 || (bm == 2 && !c.add1)) && p.K <= 2 * PADMAX + 1 && p.ntx * p.nty == 1) {
+      hipLaunchKernelGGL(k_conv_bwd_band, dim3(2 * p.B), dim3(BAND_NT),
+                         band_tile_bytes() + CONV_MISC * 4, st, c);
+      return;
+    }
+  }
   if (p.K <= 2 * PADMAX + 1)
     hipLaunchKernelGGL((k_conv_bwd<S, PADMAX, CONV_NT>), dim3(p.B), dim3(CONV_NT), (conv_lds_bytes<S, PADMAX>()), st, c);
   else
@@ -3043,7 +3160,8 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
     } else {
       if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
       ptg::Key k;
-      k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env());
+      k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
+          .add(band_env());
       rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
     }
     if (rc) return rc;

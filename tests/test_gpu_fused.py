@@ -9,7 +9,8 @@ path (read per call by the library).
 The persistent forward (k_persist_fwd, PT_CELL_PERSIST=1: all T frames of the
 fused segments in one launch, the BatchNorm syncs as in-launch waits on the
 deterministic group sums) is the same arithmetic in the same reduction order,
-so it too must reproduce the per-segment launches bit for bit."""
+so it too must reproduce the per-segment launches bit for bit.  So must the
+banded backward conv (PT_CONV_BAND=1): per output row the same MFMA order."""
 import os
 
 import pytest
@@ -25,9 +26,10 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _run(m, x, y, fused, persist=False):
+def _run(m, x, y, fused, persist=False, band=False):
     os.environ["PT_CELL_FUSED"] = "1" if fused else "0"
     os.environ["PT_CELL_PERSIST"] = "1" if persist else "0"
+    os.environ["PT_CONV_BAND"] = "1" if band else "0"
     try:
         m.zero_grad(set_to_none=True)
         out, _ = m(x)
@@ -40,6 +42,7 @@ def _run(m, x, y, fused, persist=False):
     finally:
         os.environ.pop("PT_CELL_FUSED", None)
         os.environ.pop("PT_CELL_PERSIST", None)
+        os.environ.pop("PT_CONV_BAND", None)
 
 
 @pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("int", "tanh", 5, 3),
@@ -52,6 +55,14 @@ def test_fused_forward_is_bitwise_the_split_forward(cell, act, b, t):
                                           ("hgru", "softplus", 16, 6), ("int", "softplus", 256, 64)])
 def test_persistent_forward_is_bitwise_the_fused_forward(cell, act, b, t):
     _compare(cell, act, b, t, dict(fused=True, persist=True))
+
+
+@pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("hgru", "softplus", 16, 6),
+                                          ("int", "softplus", 256, 64)])
+def test_banded_backward_conv_is_bitwise_the_whole_clip_conv(cell, act, b, t):
+    """k_conv_bwd_band (PT_CONV_BAND=1: two 16-row workgroups per clip, B
+    fragments in registers) against k_conv_bwd (one workgroup per clip)."""
+    _compare(cell, act, b, t, dict(fused=True, band=True))
 
 
 def _compare(cell, act, b, t, other):
