@@ -41,6 +41,9 @@ constexpr int SLAB_G = 6 * 1024;                 // 6 gate weights [n][ci]
 constexpr int SLAB = SLAB_G + NSMALL * 32;
 constexpr int NTRANS = 12;                       // backward transients incl. dAt, GEfin
 // BatchNorm batch sums.  PT_BN_MODE selects the reduction (compile time):
+//  3 as 2, but only the group's last member by index waits (for the
+//    others' counts, bounded poll) and sums; the others count in with a
+//    no-return atomic after their store's acknowledgement (bn_publish_finish).
 //  2 (default) bitwise reproducible, no floating-point atomics: every producer
 //    (forward: the conv workgroup of one clip / tile; backward: a point-wise
 //    workgroup) stores its 64 partial sums in its own slot with write-through
@@ -87,14 +90,40 @@ struct BnSlot {       // one (frame, BatchNorm) reduction
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-B agent-coherent (sc1) loads, as the 4-B relaxed agent-scope atomic load
+// above is lowered (there is no 16-B atomic load): eight in flight, then one
+// wait inside the same asm, so no result is read before it has landed.
+__device__ __forceinline__ void ld16_sc1x8(f32x4 (&x)[8], const f32x4* const (&p)[8]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %8, off sc1\n\t"
+      "global_load_dwordx4 %1, %9, off sc1\n\t"
+      "global_load_dwordx4 %2, %10, off sc1\n\t"
+      "global_load_dwordx4 %3, %11, off sc1\n\t"
+      "global_load_dwordx4 %4, %12, off sc1\n\t"
+      "global_load_dwordx4 %5, %13, off sc1\n\t"
+      "global_load_dwordx4 %6, %14, off sc1\n\t"
+      "global_load_dwordx4 %7, %15, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+__device__ __forceinline__ f32x4 ld16_sc1(const f32x4* p) {
+  f32x4 x;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(x) : "v"(p) : "memory");
+  return x;
+}
 
+#ifndef PT_GS_4B
+#define PT_GS_4B 0
+#endif
 // The last arriver of group g: sums of the group's partials in slot order, fp64.
 // Thread (v = tid & 63, q = tid >> 6) adds members q, q + Q, ...; the Q
 // quarter sums are then added in q order.  FWD: partial = (mean_b[32], M2_b[32])
 // -> grp = (sum mean_b, sum mean_b^2, sum M2_b); else grp = sum of the 64 values.
 // scr: NTH * (FWD ? 2 : 1) doubles of LDS.
 template <int NTH, bool FWD>
-__device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
+__device__ void bn_group_sum_4b(const BnSlot& s, int g, int tid, double* scr) {
   constexpr int Q = NTH / 64;
   const int G = bn_gsize(s.nprod), m0 = g * G, m1 = min(s.nprod, m0 + G);
   const int v = tid & 63, q = tid >> 6;
@@ -160,6 +189,84 @@ __device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
   }
 }
 
+// The last arriver of group g: sums of the group's partials, fp64, in one
+// fixed association.  Thread (v4 = tid & 15, q = tid >> 4) reads values
+// 4 v4 .. 4 v4 + 3 of members q, q + NTH/16, ... as 16-B sc1 loads, all
+// in flight at once (one round trip; the 4-byte form took four, at the tail of
+// the launch); the 4 q of a wave are added by a fixed xor butterfly, the wave
+// sums in wave order.  FWD: partial = (mean_b[32], M2_b[32]) -> grp = (sum
+// mean_b, sum mean_b^2, sum M2_b); else grp = sum of the 64 values.
+// scr: (NTH / 64) * (FWD ? 96 : 64) doubles of LDS.
+template <int NTH, bool FWD>
+__device__ void bn_group_sum(const BnSlot& s, int g, int tid, double* scr) {
+  constexpr int QW = NTH / 16, NW = NTH / 64;
+  const int G = bn_gsize(s.nprod), m0 = g * G, m1 = min(s.nprod, m0 + G);
+  const int v4 = tid & 15, q = tid >> 4, wave = tid >> 6;
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, sq[4] = {0.0, 0.0, 0.0, 0.0};
+  // G / QW at B = 256: k_pw_bb 128 / 16, k_pw_ba 32 / 16, the convs 16 / 32
+  constexpr int MAXPER = 8;
+  f32x4 xv[MAXPER];
+  const f32x4* pp[MAXPER];
+#pragma unroll
+  for (int k = 0; k < MAXPER; ++k) {
+    const int m = m0 + q + k * QW;
+    const int mc = m < m1 ? m : m0;                  // unconditional loads, masked below
+    pp[k] = (const f32x4*)(s.part + (size_t)mc * 64) + v4;
+  }
+  ld16_sc1x8(xv, pp);
+  auto add = [&](const f32x4& x) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double d = (double)x[j];
+      a[j] += d;
+      if (FWD) sq[j] += d * d;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < MAXPER; ++k)
+    if (m0 + q + k * QW < m1) add(xv[k]);
+#pragma unroll 1
+  for (int m = m0 + q + MAXPER * QW; m < m1; m += QW)   // larger groups than planned for
+    add(ld16_sc1((const f32x4*)(s.part + (size_t)m * 64) + v4));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a[j] += __shfl_xor(a[j], 16);
+    a[j] += __shfl_xor(a[j], 32);
+    if (FWD) { sq[j] += __shfl_xor(sq[j], 16); sq[j] += __shfl_xor(sq[j], 32); }
+  }
+  if ((tid & 63) < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      scr[wave * 64 + 4 * v4 + j] = a[j];
+      if (FWD && v4 < 8) scr[NW * 64 + wave * 32 + 4 * v4 + j] = sq[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      sa += scr[w * 64 + tid];
+      if (FWD && tid < 32) sb += scr[NW * 64 + w * 32 + tid];
+    }
+    double* o = s.grp + (size_t)g * (FWD ? 96 : 64);
+    auto put = [&](int i, double v) {
+      if (s.done) __hip_atomic_store(o + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else o[i] = v;
+    };
+    if (FWD) {
+      if (tid < 32) { put(tid, sa); put(32 + tid, sb); }
+      else put(32 + tid, sa);                          // sum M2_b at 64 + (tid - 32)
+    } else {
+      put(tid, sa);
+    }
+    if (s.done) {                   // the group sum is in L2: count it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) __hip_atomic_fetch_add(s.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Persistent forward: the calling WAVE waits until `target` group sums of a
 // reduction are in (its BnSlot::done counter); no workgroup barrier (the
 // caller's next one publishes what the wave then computes).  Lane 0 polls with
@@ -181,12 +288,29 @@ __device__ __forceinline__ void wave_wait(const unsigned* done, unsigned target,
 }
 
 // Producer side: this workgroup's 64 partial values (lanes tid < 64 -- wave 0
-// -- hold value tid) into the reduction.  All threads call it.  flag: an LDS
-// word no other code touches until the caller's next barrier; scr: see
-// bn_group_sum.
+// -- hold value tid) into the reduction, in two calls: bn_publish_store puts
+// the values out, bn_publish_finish completes the protocol (a caller may run
+// other work between the two; all threads call both).  flag: an LDS word no
+// other code touches until the caller's next barrier; scr: see bn_group_sum.
+//  mode 3: every member but the group's LAST by index (normally the last
+//    dispatched) waits for its store's acknowledgement and counts in with one
+//    no-return atomic -- no reply to wait for; the last member polls the count
+//    (bounded) and sums the group.  Same sums as mode 2.
+//  mode 2: every member takes a ticket (returning atomic) and the last to
+//    ARRIVE sums the group.
 template <int NTH, bool FWD>
-__device__ __forceinline__ void bn_publish(const BnSlot& s, int prod, float val, int tid, int* flag,
-                                           double* scr) {
+__device__ __forceinline__ void bn_publish_store(const BnSlot& s, int prod, float val, int tid) {
+#if PT_BN_MODE >= 2
+  if (tid < 64)
+    __hip_atomic_store(s.part + (size_t)prod * 64 + tid, val, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);                  // write-through
+#else
+  (void)s; (void)prod; (void)val; (void)tid;
+#endif
+}
+template <int NTH, bool FWD>
+__device__ __forceinline__ void bn_publish_finish(const BnSlot& s, int prod, float val, int tid, int* flag,
+                                                  double* scr) {
 #if PT_BN_MODE == 0
   if (tid < 64) {
     double* o = s.grp + (size_t)(prod % NGRP) * (FWD ? 96 : 64);
@@ -198,11 +322,32 @@ __device__ __forceinline__ void bn_publish(const BnSlot& s, int prod, float val,
 #else
   const int G = bn_gsize(s.nprod), g = prod / G;
   const int nmem = min(G, s.nprod - g * G);
+#if PT_BN_MODE == 3
+  (void)val; (void)flag;
+  if (prod != g * G + nmem - 1) {                 // a member: acknowledged, then counted
+    if (tid < 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) __hip_atomic_fetch_add(s.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (tid < 64) {                                 // the group's last member
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0)
+      for (unsigned it = 0; it < (1u << 22); ++it) {   // ~0.3 s bound: never a hang
+        if (__hip_atomic_load(s.cnt + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)(nmem - 1))
+          break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+  }
+  __syncthreads();
+  bn_group_sum<NTH, FWD>(s, g, tid, scr);
+#else
   if (tid < 64) {
 #if PT_BN_MODE == 2
-    __hip_atomic_store(s.part + (size_t)prod * 64 + tid, val, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);                  // write-through
+#ifndef PT_BN_NOWAIT
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this wave's payload is in L2
+#endif
     if (tid == 0) {
       const unsigned old = __hip_atomic_fetch_add(s.cnt + g, 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -226,8 +371,18 @@ __device__ __forceinline__ void bn_publish(const BnSlot& s, int prod, float val,
 #endif
   }
   __syncthreads();
-  if (*flag) bn_group_sum<NTH, FWD>(s, g, tid, scr);
+  if (*flag) {
+    if (PT_GS_4B) bn_group_sum_4b<NTH, FWD>(s, g, tid, scr);
+    else bn_group_sum<NTH, FWD>(s, g, tid, scr);
+  }
 #endif
+#endif
+}
+template <int NTH, bool FWD>
+__device__ __forceinline__ void bn_publish(const BnSlot& s, int prod, float val, int tid, int* flag,
+                                           double* scr) {
+  bn_publish_store<NTH, FWD>(s, prod, val, tid);
+  bn_publish_finish<NTH, FWD>(s, prod, val, tid, flag, scr);
 }
 
 // ----------------------------------------------------------------- arguments
@@ -452,9 +607,18 @@ __device__ void bn_fwd_finalize(const double* __restrict__ grp, int ng, int B, f
     auto ld = [&](int i) {
       return COH ? __hip_atomic_load(grp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : grp[i];
     };
-    for (int k = 0; k < ng; ++k) {
-      s1 += ld(k * 96 + tid); s2 += ld(k * 96 + 32 + tid); s3 += ld(k * 96 + 64 + tid);
+    // every group's loads in flight at once, then added in group order (a
+    // loop over the runtime count waited on each group in turn: ~5.5 us of
+    // the consumer's prologue)
+    double x1[NGRP], x2[NGRP], x3[NGRP];
+#pragma unroll
+    for (int k = 0; k < NGRP; ++k) {
+      const int kk = k < ng ? k : 0;
+      x1[k] = ld(kk * 96 + tid); x2[k] = ld(kk * 96 + 32 + tid); x3[k] = ld(kk * 96 + 64 + tid);
     }
+#pragma unroll
+    for (int k = 0; k < NGRP; ++k)
+      if (k < ng) { s1 += x1[k]; s2 += x2[k]; s3 += x3[k]; }
     const double mean = s1 / B;
     double m2 = s3 + (double)NPIX * (s2 - s1 * s1 / B);
     m2 = m2 > 0.0 ? m2 : 0.0;
@@ -471,16 +635,18 @@ __device__ void bn_fwd_finalize(const double* __restrict__ grp, int ng, int B, f
 // RW rows (its per-channel means go through its own LDS slot, no workgroup
 // barrier); one barrier, then Chan's combination over the NW equal-sized wave
 // blocks: M2 = sum M2_w + n_w sum (mean_w - mean)^2.  red: 2 * NW * 32 floats.
+// Block blk (RW rows held in acc by the calling wave): two-pass per-channel
+// mean -> red[blk * 32 + ch], M2 -> red[NW * 32 + blk * 32 + ch] (the block's
+// means go through its own LDS slot: no workgroup barrier).
 template <int RW, int NW>
-__device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, const BnSlot& out, int prod,
-                               int lane, int wave, int tid, int ablate, int* flag, double* scr) {
+__device__ __forceinline__ void bn_block_stats(const f32x16 (&acc)[RW], float* red, int blk, int lane) {
   const int h = lane >> 5;
   const int ch = pl_ch(pl_sum_reg(lane), h);
   f32x16 s = acc[0];
 #pragma unroll
   for (int i = 1; i < RW; ++i) s += acc[i];
   const float ts = pl_lane_sum(s, lane);
-  float* rw = red + wave * 32;                       // this wave's block means
+  float* rw = red + blk * 32;                        // this block's means
   if (!(lane & 16)) rw[ch] = ts * (1.f / (RW * IMG));
   wave_sync();
   f32x16 mean;
@@ -497,10 +663,15 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, const BnSlot
     q += d * d;
   }
   const float tq = pl_lane_sum(q, lane);
-  if (!(lane & 16)) red[NW * 32 + wave * 32 + ch] = tq;
-  __syncthreads();
-  if (ablate & 32768) return;
-  // lanes 0-31: channel tid's block mean; lanes 32-63: its M2 (Chan over the NW wave blocks)
+  if (!(lane & 16)) red[NW * 32 + blk * 32 + ch] = tq;
+}
+// After a workgroup barrier: Chan's combination over the NW equal-sized blocks
+// (M2 = sum M2_w + n_w sum (mean_w - mean)^2), published to the batch
+// reduction.  All NW * 64 threads call it.
+template <int RW, int NW>
+__device__ __forceinline__ void bn_blocks_publish(const float* red, const BnSlot& out, int prod, int tid,
+                                                  int* flag, double* scr) {
+  // lanes 0-31: channel tid's block mean; lanes 32-63: its M2
   const int ch2 = tid & 31;
   float mn = 0.f;
 #pragma unroll
@@ -515,6 +686,18 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, const BnSlot
   }
   v += dv * (float)(RW * IMG);
   bn_publish<NW * 64, true>(out, prod, tid < 32 ? mn : v, tid, flag, scr);
+}
+// Per-clip (mean, M2) of the conv outputs held in acc (PL layout), published
+// to the deterministic batch reduction (bn_publish; scr / flag: free LDS): each
+// wave's RW rows are one block (bn_block_stats), one barrier, then the
+// combination (bn_blocks_publish).  red: 2 * NW * 32 floats.
+template <int RW, int NW>
+__device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, const BnSlot& out, int prod,
+                               int lane, int wave, int tid, int ablate, int* flag, double* scr) {
+  bn_block_stats<RW, NW>(acc, red, wave, lane);
+  __syncthreads();
+  if (ablate & 32768) return;
+  bn_blocks_publish<RW, NW>(red, out, prod, tid, flag, scr);
 }
 
 // =========================================================================
@@ -531,6 +714,21 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, const BnSlot
 // =========================================================================
 enum { FILL_COPY = 0, FILL_BNBWD = 1 };
 enum { EPI_FWD = 0, EPI_ADD = 1, EPI_NONE = 2 };
+
+// Backward BN consumers: sum dy and sum dy*xhat of channel c over the ng (<=
+// NGRP) group sums, added in group order with every load in flight at once.
+__device__ __forceinline__ void bnb_sums(const double* __restrict__ g, int ng, int c, double& sd, double& sdx) {
+  double x[NGRP], y[NGRP];
+#pragma unroll
+  for (int k = 0; k < NGRP; ++k) {
+    const int kk = k < ng ? k : 0;
+    x[k] = g[kk * 64 + c];
+    y[k] = g[kk * 64 + 32 + c];
+  }
+#pragma unroll
+  for (int k = 0; k < NGRP; ++k)
+    if (k < ng) { sd += x[k]; sdx += y[k]; }
+}
 
 template <class S>
 struct ConvArgs {
@@ -636,7 +834,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       // dx = A dy + Bc raw + Cc  with A = rstd g, xhat = (raw - mean) rstd
       const double inv = 1.0 / ((double)a.bnB * NPIX);
       double sd = 0.0, sdx = 0.0;
-      for (int k = 0; k < a.bnb_ngrp; ++k) { sd += a.bnb[k * 64 + tid]; sdx += a.bnb[k * 64 + 32 + tid]; }
+      bnb_sums(a.bnb, a.bnb_ngrp, tid, sd, sdx);
       const float md = (float)(sd * inv), mdx = (float)(sdx * inv);
       const float mean = a.bnstat[tid], rstd = a.bnstat[32 + tid];
       const float A = rstd * a.bnw[tid];
@@ -822,7 +1020,7 @@ __global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a
   if (tid < 32) {     // BN backward as an affine map per channel (as conv_body)
     const double inv = 1.0 / ((double)a.bnB * NPIX);
     double sd = 0.0, sdx = 0.0;
-    for (int k = 0; k < a.bnb_ngrp; ++k) { sd += a.bnb[k * 64 + tid]; sdx += a.bnb[k * 64 + 32 + tid]; }
+    bnb_sums(a.bnb, a.bnb_ngrp, tid, sd, sdx);
     const float md = (float)(sd * inv), mdx = (float)(sdx * inv);
     const float mean = a.bnstat[tid], rstd = a.bnstat[32 + tid];
     const float A = rstd * a.bnw[tid];
@@ -1104,8 +1302,10 @@ __device__ void flush_small(float (&v)[N], const int (&slot)[N], float* small, c
 // Workgroup totals of two per-lane channel sums -> the deterministic batch
 // reduction (bn_publish).  red: 512 floats (reused as the group-sum scratch);
 // flag: an LDS word outside red.
-__device__ void bn_bwd_partial(float s0, float s1, float* red, const BnSlot& out, int lane,
-                               int wave, int tid, int* flag) {
+// The caller completes the protocol (bn_publish_finish with the returned value)
+// after its slab flush: the partial's store latency hides under the flush.
+__device__ float bn_bwd_partial(float s0, float s1, float* red, const BnSlot& out, int lane,
+                                int wave, int tid) {
   s0 += __shfl_xor(s0, 32);
   s1 += __shfl_xor(s1, 32);
   if (lane < 32) { red[wave * 32 + lane] = s0; red[256 + wave * 32 + lane] = s1; }
@@ -1116,8 +1316,8 @@ __device__ void bn_bwd_partial(float s0, float s1, float* red, const BnSlot& out
 #pragma unroll
     for (int w = 0; w < PW_NW; ++w) a += red[o + w * 32];
   }
-  bn_publish<PW_NT, false>(out, blockIdx.x, a, tid, flag, (double*)red);
-  __syncthreads();
+  bn_publish_store<PW_NT, false>(out, blockIdx.x, a, tid);
+  return a;
 }
 
 // -------------------------------------------------------------------------
@@ -1390,7 +1590,8 @@ __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<
   const StoreRow<S> sr{out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h};
   auto nofill = [](int) {};                 // the point-wise half filled the tile
   conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
-                                   tid, 0, sr);
+                                   tid, a.ablate & 1, sr);
+  if (a.ablate & 8) return;
   bn_fwd_partial<RW, FUSED_NW>(acc, L.red, bnout, b, lane, wave, tid, 0,
                                (int*)(smem + CONV_NT * 16), (double*)smem);
 }
@@ -1408,13 +1609,13 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
   // persistent: only the finalising wave waits for the batch sums (COH); the
   // others' row loads and the x staging below go out meanwhile
   if (COH && wave == FUSED_NW - 1 && t > 0) wave_wait(wcnt, wtarget, err, lane);
-  if (wave == FUSED_NW - 1 && t > 0)
+  if (!(a.ablate & 65536) && wave == FUSED_NW - 1 && t > 0)
     bn_fwd_finalize<COH>(bnf_src(a, t - 1, 1), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat + 64,
                          b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   // this wave's first row's tiles go out before the staging and the barrier
   FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
-  stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  if (!(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
 #pragma unroll 1
   for (int i = 0; i < FUSED_RW; ++i) {
@@ -1422,8 +1623,9 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
     const size_t ro = clip_off(b) + (size_t)y * IMG * C;
     const FaIn<S> cur = nxt;
     if (i + 1 < FUSED_RW) nxt = fa_load(a, t, ro + (size_t)IMG * C, cl, h);   // next row in flight
-    fa_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
-                       (S*)L.tile);
+    if (!(a.ablate & 4))
+      fa_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
+                         (S*)L.tile);
   }
   fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
 }
@@ -1439,12 +1641,12 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
   const int b = blockIdx.x;
   if constexpr (COH) __syncthreads();
   if (COH && wave == FUSED_NW - 1) wave_wait(wcnt, wtarget, err, lane);
-  if (wave == FUSED_NW - 1)
+  if (!(a.ablate & 65536) && wave == FUSED_NW - 1)
     bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
                          b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
   FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
-  stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  if (!(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
 #pragma unroll 1
   for (int i = 0; i < FUSED_RW; ++i) {
@@ -1452,8 +1654,9 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     const size_t ro = clip_off(b) + (size_t)y * IMG * C;
     const FbIn<S> cur = nxt;
     if (i + 1 < FUSED_RW) nxt = fb_load<S, HG>(a, t, ro + (size_t)IMG * C, cl, h);
-    fb_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
-                       (S*)L.tile);
+    if (!(a.ablate & 4))
+      fb_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
+                         (S*)L.tile);
   }
   fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
 }
@@ -1636,10 +1839,14 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
-  if (head && !(a.ablate & 8))   // L.stat is unused by the backward kernels: the ticket's flag word
-    bn_bwd_partial(bs0, bs1, L.red, bnb_slot(a, t, 1, B * PWA_WGPC), lane, wave, tid, (int*)L.stat);
+  const bool bn = head && !(a.ablate & 8);
+  const BnSlot bo = bnb_slot(a, t, 1, B * PWA_WGPC);
+  float bv = 0.f;
+  if (bn) bv = bn_bwd_partial(bs0, bs1, L.red, bo, lane, wave, tid);
   if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
   if (tail && (head || HG) && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
+  // L.stat is unused by the backward kernels: mode 2's ticket flag word
+  if (bn) bn_publish_finish<PW_NT, false>(bo, blockIdx.x, bv, tid, (int*)L.stat, (double*)L.red);
 }
 template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
@@ -1837,10 +2044,13 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   }
   sm[4] = bs1;
   sm[5] = bs0;
-  if (!a.no_inh && !(a.ablate & 8))
-    bn_bwd_partial(bs0, bs1, L.red, bnb_slot(a, t, 0, B * PWB_WGPC), lane, wave, tid, (int*)L.stat);
+  const bool bn = !a.no_inh && !(a.ablate & 8);
+  const BnSlot bo = bnb_slot(a, t, 0, B * PWB_WGPC);
+  float bv = 0.f;
+  if (bn) bv = bn_bwd_partial(bs0, bs1, L.red, bo, lane, wave, tid);
+  if (!(a.ablate & 32)) flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
+  if (bn) bn_publish_finish<PW_NT, false>(bo, blockIdx.x, bv, tid, (int*)L.stat, (double*)L.red);
   if (a.ablate & 32) return;
-  flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5 (bf16: written by gate_wgrad)
   if constexpr (!BF) {
     if (!a.no_inh) gacc_flush(L.gacc, L.slabl, slab_p, 2, 2, tid);

@@ -31,6 +31,8 @@ LIBS = {
                       os.path.join(INC, "pt_lstm.h")]),
 }
 OUT = os.path.join(HERE, "libptcell.so")      # kept for callers of the old single-library API
+# The compiler line of the HIP libraries; part of the source stamp.
+HIP_FLAGS = "--offload-arch=gfx950 -O3 -std=c++17"
 
 
 def _out(lib: str) -> str:
@@ -50,7 +52,7 @@ def src_hash(lib: str) -> str:
     """sha256 (first 12 hex digits) of a library's sources and headers: compiled
     into its version string, so measurements (profiles/*_pmc_traffic.json) can
     be matched to the exact kernels that produced them."""
-    h = hashlib.sha256()
+    h = hashlib.sha256(HIP_FLAGS.encode())
     srcs, deps = LIBS[lib]
     for f in srcs + deps:
         h.update(os.path.basename(f).encode())
@@ -70,7 +72,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
             cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared",
                    "-pthread", "-Wall", "-I", INC, "-o", out + ".tmp", *srcs, "-lz", "-ldl"]
         else:
-            cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+            cmd = [hipcc, *HIP_FLAGS.split(), "-fPIC", "-shared",
                    f'-DPT_SRC_HASH="{src_hash(lib)}"', "-I", INC, "-o", out + ".tmp", *srcs]
         if verbose:
             print(" ".join(cmd), flush=True)
