@@ -64,7 +64,15 @@ __device__ void ro_planes(const RoArgs& a, int b, float* z, int tid) {
   for (int p = tid; p < HW; p += RO_NT) {
     const int y = p / a.W, x = p - y * a.W;
     float r = cb;
-    for (int c = 0; c < a.C; ++c) r += a.p.conv_w[c] * eb[(size_t)c * HW + p];
+    int c = 0;
+    for (; c + 8 <= a.C; c += 8) {       // 8 channel loads in flight, then added in order
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = eb[(size_t)(c + k) * HW + p];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r += a.p.conv_w[c + k] * v[k];
+    }
+    for (; c < a.C; ++c) r += a.p.conv_w[c] * eb[(size_t)c * HW + p];
     z[(y + 2) * PW + x + 2] = r;
     z[PH * PW + (y + 2) * PW + x + 2] = a.tgt[(size_t)b * HW + p];
   }
@@ -151,16 +159,47 @@ __global__ __launch_bounds__(RO_NT) void k_ro_bwd(RoArgs a) {
   __syncthreads();
   const float* eb = a.e + (size_t)b * C * HW;
   float* deb = a.d_e + (size_t)b * C * HW;
-  for (int c = 0; c < C; ++c) {
+  auto chan = [&](int c, const float (&ev)[4]) {    // ev: this thread's E[c][tid + k RO_NT], k < 4
     const float wc = a.p.conv_w[c];
     float g = 0.f;
-    for (int p = tid; p < HW; p += RO_NT) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = tid + k * RO_NT;
+      if (p < HW) {
+        const float dr = drs[p];
+        g += dr * ev[k];
+        deb[(size_t)c * HW + p] = wc * dr;
+      }
+    }
+    for (int p = tid + 4 * RO_NT; p < HW; p += RO_NT) {
       const float dr = drs[p];
       g += dr * eb[(size_t)c * HW + p];
       deb[(size_t)c * HW + p] = wc * dr;
     }
     g = wave_sum(g);
     if (lane == 0) wred[c * NW + wave] = g;
+  };
+  int c0 = 0;
+  for (; c0 + 4 <= C; c0 += 4) {        // the first 4 pixels of 4 channels in flight at once
+    float ev[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = tid + k * RO_NT;
+        ev[j][k] = p < HW ? eb[(size_t)(c0 + j) * HW + p] : 0.f;
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) chan(c0 + j, ev[j]);
+  }
+  for (; c0 < C; ++c0) {
+    float ev[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = tid + k * RO_NT;
+      ev[k] = p < HW ? eb[(size_t)c0 * HW + p] : 0.f;
+    }
+    chan(c0, ev);
   }
   gcb = wave_sum(gcb);
   if (lane == 0) wred[C * NW + wave] = gcb;
@@ -189,7 +228,15 @@ __global__ void k_ro_reduce(RoArgs a, pt_readout_grads g) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x, C = a.C, np = ro_npar(C);
   if (j >= np) return;
   float s = 0.f;
-  for (int b = 0; b < a.B; ++b) s += a.part[(size_t)b * np + j];
+  int b = 0;
+  for (; b + 32 <= a.B; b += 32) {       // 32 loads in flight, added in clip order
+    float v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = a.part[(size_t)(b + k) * np + j];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) s += v[k];
+  }
+  for (; b < a.B; ++b) s += a.part[(size_t)b * np + j];
   if (j < C) g.conv_w[j] = s;
   else if (j == C) g.conv_b[0] = s;
   else if (j < C + 51) g.target_w[j - C - 1] = s;
