@@ -170,6 +170,12 @@ int pt_cell_timing_enable(uint32_t kind_mask);      /* bit k enables kind k; 0 d
 int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches);
 int pt_cell_timing_reset(void);
 
+/* Diagnostics: per-workgroup phase stamps (100 MHz real-time counter) of the
+ * launches of frame `frame`, written to buf as u64 [PT_K_NKINDS][256][16]
+ * (workgroups < 256; slot meanings in csrc/pt_cell.hip, PT_TR).  buf = NULL
+ * turns it off.  hipGraph replay is off while a buffer is set. */
+int pt_cell_trace(void* buf, int frame);
+
 const char* pt_last_error(void);
 const char* pt_version(void);
 

@@ -396,6 +396,8 @@ struct CellArgs {
   int t;
   int ntx, nty;   // frames of (32 nty) x (32 ntx) px as nty x ntx tiles of 32x32 ("virtual
                   // clips": B counts tiles, B = clips * ntx * nty); 1 x 1 at 32x32
+  unsigned long long* trace;   // diagnostics (pt_cell_trace): per-workgroup phase stamps of frame trace_t
+  int trace_t;
   int ablate;     // timing experiments only (env PT_CELL_ABLATE): 1 skip conv MFMAs,
                   // 256 skip the conv epilogue, 512 return at entry (launch floor),
                   // 2 skip tile fill, 4 skip point-wise row loops, 8 skip BN fp64
@@ -444,6 +446,18 @@ struct CellArgs {
   int conv_done;                        // k_pw_ba: dgE holds conv^T(w_inh) + dgEp
 };
 
+// Phase stamp (diagnostics, pt_cell_trace): thread 0 of every (gridDim.x / 256)-th
+// workgroup of the traced frame writes the 100 MHz real-time counter into slot
+// `slot` (< 16) of its record trace[kind][blockIdx.x / stride][16].  Off (a
+// null pointer) in every normal run.
+#define PT_TR(a, kind, slot)                                                                   \
+  do {                                                                                         \
+    const unsigned tr_s_ = gridDim.x > 256 ? gridDim.x / 256 : 1;                              \
+    if ((a).trace && (a).t == (a).trace_t && threadIdx.x == 0 && blockIdx.x % tr_s_ == 0 &&     \
+        blockIdx.x / tr_s_ < 256)                                                               \
+      (a).trace[((size_t)(kind) * 256 + blockIdx.x / tr_s_) * 16 + (slot)] =                     \
+          __builtin_amdgcn_s_memrealtime();                                                     \
+  } while (0)
 __device__ __forceinline__ size_t fr_off(int t, int B) { return (size_t)t * B * NPIX * C; }
 
 // (frame t, BatchNorm bn) reduction slots; nprod of the backward ones: the
@@ -1605,6 +1619,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
   const int lane = tid & 63, cl = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
+  PT_TR(a, PT_K_FUSED_FA, 0);
   if constexpr (COH) __syncthreads();      // the previous segment's LDS use is over
   // persistent: only the finalising wave waits for the batch sums (COH); the
   // others' row loads and the x staging below go out meanwhile
@@ -1617,6 +1632,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
   if (!(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
+  PT_TR(a, PT_K_FUSED_FA, 2);
 #pragma unroll 1
   for (int i = 0; i < FUSED_RW; ++i) {
     const int y = wave * FUSED_RW + i;
@@ -1627,7 +1643,9 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
       fa_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
                          (S*)L.tile);
   }
+  PT_TR(a, PT_K_FUSED_FA, 3);
   fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
+  PT_TR(a, PT_K_FUSED_FA, 6);
 }
 
 template <class S, int ACT, int HG, bool COH>
@@ -1639,6 +1657,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
   const int lane = tid & 63, cl = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
+  PT_TR(a, PT_K_FUSED_FB, 0);
   if constexpr (COH) __syncthreads();
   if (COH && wave == FUSED_NW - 1) wave_wait(wcnt, wtarget, err, lane);
   if (!(a.ablate & 65536) && wave == FUSED_NW - 1)
@@ -1648,6 +1667,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
   if (!(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
+  PT_TR(a, PT_K_FUSED_FB, 2);
 #pragma unroll 1
   for (int i = 0; i < FUSED_RW; ++i) {
     const int y = wave * FUSED_RW + i;
@@ -1658,7 +1678,9 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
       fb_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
                          (S*)L.tile);
   }
+  PT_TR(a, PT_K_FUSED_FB, 3);
   fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
+  PT_TR(a, PT_K_FUSED_FB, 6);
 }
 
 template <class S, int ACT, int HG>
@@ -1735,10 +1757,12 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   const bool tail = tt <= T - 1, head = t >= 0;
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
+  PT_TR(a, PT_K_PW_BA, 0);
   slab_prefetch(slab_p, L.slabl, 0, 2, wave, lane);        // a_w, a_u
   if (tail) stage_x(a.x, a.xu8, L.xs, b, tt, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   gacc_zero(L.gacc, 2, tid);
   __syncthreads();
+  PT_TR(a, PT_K_PW_BA, 2);
 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
   float sm[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1839,14 +1863,18 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
+  PT_TR(a, PT_K_PW_BA, 3);
   const bool bn = head && !(a.ablate & 8);
   const BnSlot bo = bnb_slot(a, t, 1, B * PWA_WGPC);
   float bv = 0.f;
   if (bn) bv = bn_bwd_partial(bs0, bs1, L.red, bo, lane, wave, tid);
+  PT_TR(a, PT_K_PW_BA, 4);
   if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
   if (tail && (head || HG) && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
+  PT_TR(a, PT_K_PW_BA, 5);
   // L.stat is unused by the backward kernels: mode 2's ticket flag word
   if (bn) bn_publish_finish<PW_NT, false>(bo, blockIdx.x, bv, tid, (int*)L.stat, (double*)L.red);
+  PT_TR(a, PT_K_PW_BA, 6);
 }
 template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
@@ -1884,7 +1912,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   // d_e_pre is folded into dI_{t-1} at the end from its A fragments (pe)
   // rather than kept as a tile.  hGRU: g_inh = att_t (ffhgru_hierarchy.py:147)
   // and I_{t-1} is a separate tile.
-  auto load_row = [&](size_t ro) {
+  auto load_row = [&](size_t ro, int c, int h) {
     BbRow<S> w;
     w.Iprev = zero_pk<S>();
     if constexpr (HG) {
@@ -1905,19 +1933,18 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
     }
     return w;
   };
+  PT_TR(a, PT_K_PW_BB, 0);
   // one row per wave: its tiles are loaded first, their latency overlaps the staging
   BbRow<S> pre;
-  if constexpr (RPP == 1) pre = load_row(clip_off(b) + (size_t)(y0 + wave) * IMG * C);
+  if constexpr (RPP == 1) pre = load_row(clip_off(b) + (size_t)(y0 + wave) * IMG * C, c, h);
   if (!(a.ablate & 262144)) slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);   // i_w, i_u, e_w, e_u
   stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   if constexpr (!BF) gacc_zero(L.gacc, 4, tid);
+  PT_TR(a, PT_K_PW_BB, 1);
   __syncthreads();
+  PT_TR(a, PT_K_PW_BB, 2);
 
   const float* bs = a.bnstat + (size_t)t * 128;
-  const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
-  const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
-  const float m0 = bs[c], rs0 = bs[32 + c];
-  const float nbi = sig_nb(a.gb[2][c] + a.gb[3][c]);
   float sm[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int slots[10] = {SM_ALPHA, SM_MU, SM_GBI, SM_GBE, SM_BN0W, SM_BN0B,
                          SM_PW0, SM_PW1, SM_PW2, SM_PB};
@@ -1925,11 +1952,21 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
 
 #pragma unroll 1
   for (int i = 0; i < RPP && !(a.ablate & 4); ++i) {
+    // several rows per wave: the lane index laundered per row, so that the
+    // per-lane parameters and addresses are formed in the row instead of
+    // staying live across the loop as invariants (RPP 2: 161 VGPRs of spills)
+    int tl = tid;
+    if constexpr (RPP > 1) asm volatile("" : "+v"(tl));
+    const int lane = tl & 63, c = lane & 31, h = lane >> 5;
+    const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
+    const float al = a.alpha[c], mu = a.mu[c], bw0 = a.bnw0[c], bb0 = a.bnb0[c];
+    const float m0 = bs[c], rs0 = bs[32 + c];
+    const float nbi = sig_nb(a.gb[2][c] + a.gb[3][c]);
     const int yl = wave * RPP + i, y = y0 + yl;
     const size_t ro = clip_off(b) + (size_t)y * IMG * C;
     BbRow<S> w;
     if constexpr (RPP == 1) w = pre;
-    else w = load_row(ro);
+    else w = load_row(ro, c, h);
     const Pk<S>& ginh = w.ginh;
     const Pk<S>& dIt = w.dIt;
     const Pk<S>& civ = w.civ;
@@ -2044,12 +2081,16 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   }
   sm[4] = bs1;
   sm[5] = bs0;
+  PT_TR(a, PT_K_PW_BB, 3);
   const bool bn = !a.no_inh && !(a.ablate & 8);
   const BnSlot bo = bnb_slot(a, t, 0, B * PWB_WGPC);
   float bv = 0.f;
   if (bn) bv = bn_bwd_partial(bs0, bs1, L.red, bo, lane, wave, tid);
+  PT_TR(a, PT_K_PW_BB, 4);
   if (!(a.ablate & 32)) flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
+  PT_TR(a, PT_K_PW_BB, 5);
   if (bn) bn_publish_finish<PW_NT, false>(bo, blockIdx.x, bv, tid, (int*)L.stat, (double*)L.red);
+  PT_TR(a, PT_K_PW_BB, 6);
   if (a.ablate & 32) return;
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5 (bf16: written by gate_wgrad)
   if constexpr (!BF) {
@@ -2737,6 +2778,9 @@ struct Timing {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
 };
 Timing g_tm;
+// pt_cell_trace: phase stamps of one frame's launches (diagnostics)
+unsigned long long* g_trace = nullptr;
+int g_trace_t = -1;
 
 hipEvent_t tm_event() {
   if (g_tm.used == g_tm.pool.size()) {
@@ -2855,6 +2899,8 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   a.ntx = p.ntx; a.nty = p.nty;
   a.hgru = d->cell == PT_CELL_HGRU;
   a.bn_world = 1;
+  a.trace = g_trace;
+  a.trace_t = g_trace_t;
   a.x = x;
   a.xu8 = d->x_format == PT_X_U8_NTHWC;
   {
@@ -3285,7 +3331,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
 ptg::GraphCache g_graphs;
 bool use_graph() {
   return ptg::graphs_enabled() && __atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) == 0 &&
-         !getenv("PT_CELL_DEBUG_STOP");
+         !getenv("PT_CELL_DEBUG_STOP") && !g_trace;
 }
 int ablate_env() {
   const char* ab = getenv("PT_CELL_ABLATE");
@@ -3384,6 +3430,12 @@ int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params*
                      const void* saved, void* ws, const float* d_e_last, const pt_cell_grads* g,
                      pt_stream_t stream) {
   return pt_cell_backward_dist(d, x, p, saved, ws, d_e_last, g, nullptr, stream);
+}
+
+int pt_cell_trace(void* buf, int frame) {
+  g_trace = (unsigned long long*)buf;
+  g_trace_t = frame;
+  return 0;
 }
 
 int pt_cell_timing_enable(uint32_t kind_mask) {

@@ -22,7 +22,7 @@ PT_X_F32_NCTHW, PT_X_U8_NTHWC = 0, 1
 EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
            "pt_cell_export_exc", "pt_cell_backward", "pt_cell_bn_sync_doubles",
            "pt_cell_forward_dist", "pt_cell_backward_dist", "pt_cell_timing_enable",
-           "pt_cell_timing_read", "pt_cell_timing_reset", "pt_last_error", "pt_version")
+           "pt_cell_timing_read", "pt_cell_timing_reset", "pt_cell_trace", "pt_last_error", "pt_version")
 
 # kernel kinds for pt_cell_timing_* (include/pt_cell.h)
 KIND_NAMES = ("k_pw_fa", "k_conv_fa", "k_pw_fb", "k_conv_fb", "k_pw_ba", "k_conv_ba",
@@ -107,6 +107,8 @@ def load():
         lib.pt_cell_timing_read.restype = ctypes.c_int
         lib.pt_cell_timing_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_int64)]
+        lib.pt_cell_trace.restype = ctypes.c_int
+        lib.pt_cell_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.pt_cell_timing_reset.restype = ctypes.c_int
         lib.pt_last_error.restype = ctypes.c_char_p
         lib.pt_version.restype = ctypes.c_char_p
