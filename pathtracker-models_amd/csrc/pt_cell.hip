@@ -1595,7 +1595,7 @@ __device__ __forceinline__ FusedLds fused_carve(char* smem) {
 template <class S>
 __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<S>& c, S* out_raw,
                                            const BnSlot& bnout, char* smem, const FusedLds& L, int b,
-                                           int wave, int lane, int tid) {
+                                           int wave, int lane, int tid, int kind) {
   constexpr int RW = FUSED_RW;
   f32x16 acc[RW];
 #pragma unroll
@@ -1605,9 +1605,12 @@ __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<
   auto nofill = [](int) {};                 // the point-wise half filled the tile
   conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
                                    tid, a.ablate & 1, sr);
+  PT_TR(a, kind, 4);
   if (a.ablate & 8) return;
-  bn_fwd_partial<RW, FUSED_NW>(acc, L.red, bnout, b, lane, wave, tid, 0,
-                               (int*)(smem + CONV_NT * 16), (double*)smem);
+  bn_block_stats<RW, FUSED_NW>(acc, L.red, wave, lane);       // = bn_fwd_partial, stamped
+  __syncthreads();
+  PT_TR(a, kind, 5);
+  bn_blocks_publish<RW, FUSED_NW>(L.red, bnout, b, tid, (int*)(smem + CONV_NT * 16), (double*)smem);
 }
 
 template <class S, int ACT, int HG, bool COH>
@@ -1644,7 +1647,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
                          (S*)L.tile);
   }
   PT_TR(a, PT_K_FUSED_FA, 3);
-  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
+  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FA);
   PT_TR(a, PT_K_FUSED_FA, 6);
 }
 
@@ -1679,7 +1682,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
                          (S*)L.tile);
   }
   PT_TR(a, PT_K_FUSED_FB, 3);
-  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid);
+  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FB);
   PT_TR(a, PT_K_FUSED_FB, 6);
 }
 

@@ -16,8 +16,8 @@ from models import InT  # noqa: E402
 
 SLOTS = {"k_pw_bb": ["entry", "issued", "prologue", "rows", "bn_partial", "flush", "publish"],
          "k_pw_ba": ["entry", "-", "prologue", "rows", "bn_partial", "flush", "publish"],
-         "k_fused_fa": ["entry", "-", "prologue", "pw_rows", "-", "-", "conv+bn"],
-         "k_fused_fb": ["entry", "-", "prologue", "pw_rows", "-", "-", "conv+bn"]}
+         "k_fused_fa": ["entry", "-", "prologue", "pw_rows", "conv", "bn_stats", "bn_publish"],
+         "k_fused_fb": ["entry", "-", "prologue", "pw_rows", "conv", "bn_stats", "bn_publish"]}
 
 
 def main():
