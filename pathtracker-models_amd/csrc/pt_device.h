@@ -486,8 +486,18 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
 #ifndef CONV_PF
 #define CONV_PF 3                    // A-fragment prefetch depth (tile rows)
 #endif
+#ifndef CONV_PF_W
+#define CONV_PF_W 5                  // the same for the register-weight (WREG) flat pipeline
+#endif
+// 1 (default): one software pipeline over all (kernel column, tile row) steps
+// of a bf16 conv, the A fragments CONV_PF(_W) steps ahead across column
+// boundaries too; 0: a pipeline per column, drained at every column's end.
+// Same MFMA order per accumulator (bitwise equal).  Measured (interleaved,
+// B=256 T=64): fused fa / fb 73.8 / 51.9 -> 72.7 / 51.4 us, conv_ba / conv_bb
+// 34.0 / 38.6 -> 33.3 / 37.9 us; A depth 5 on the register-weight path
+// another -0.6 / -0.4 us on fa / fb (6 lost on conv_ba).
 #ifndef PT_CONV_FLAT
-#define PT_CONV_FLAT 0               // 1: one (column, row) pipeline for the register-weight convs
+#define PT_CONV_FLAT 1
 #endif
 constexpr int WSLICE_CHUNKS = 896;   // 16-B chunks per slice: 7 taps x 2 x 64 x 16 B (bf16)
                                      //                       = 7 taps x 8 x 64 x 4 B (f32, per pass)
@@ -600,7 +610,7 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
     __syncthreads();
     if (ablate & 1) return;
     constexpr int NST = K * NTR;
-    constexpr int PF = CONV_PF < NST ? CONV_PF : NST;
+    constexpr int PF = CONV_PF_W < NST ? CONV_PF_W : NST;
     F av[PF + 1][KSP];
     auto load_step = [&](int st) {
       const int kw = st / NTR, tr = st - kw * NTR;
