@@ -183,8 +183,11 @@ def make_data(seed, batch, frames, device, u8=False):
     clip bytes [B,T,32,32,3] the cell converts while staging each frame."""
     from ptamd import synth
     clips, labels = synth.make_batch(seed, batch, frames)
+    # C-contiguous [B,3,T,H,W] as prepare_data hands it over (the transposed
+    # numpy view kept its strides through astype / .to(device), and the cell
+    # then made a 201 MB contiguous copy inside every timed step: 81 us)
     x = (torch.from_numpy(clips) if u8 else
-         torch.from_numpy(clips.transpose(0, 4, 1, 2, 3).astype(np.float32) / 255.0))
+         torch.from_numpy(np.ascontiguousarray(clips.transpose(0, 4, 1, 2, 3), dtype=np.float32) / 255.0))
     y = torch.tensor([ord(b) for b in labels], dtype=torch.float32)
     return x.to(device), y.to(device)
 
