@@ -297,7 +297,9 @@ def main():
         if world > 1:
             model.cell_dist = CellDist(sync_bn=args.sync_bn,
                                        bucket=None if args.no_grad_overlap else bucket)
-        return model, bucket, torch.optim.Adam(model.parameters(), lr=3e-4)
+        # the same Adam update as one fused kernel over all parameters (the
+        # default multi-tensor form launched seven kernels, ~0.1 ms per step)
+        return model, bucket, torch.optim.Adam(model.parameters(), lr=3e-4, fused=True)
 
     model, bucket, opt = build(args.dtype)
     crit = torch.nn.BCEWithLogitsLoss()
