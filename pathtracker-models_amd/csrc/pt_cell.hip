@@ -3024,12 +3024,15 @@ void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   else
     hipLaunchKernelGGL((k_conv_fwd<S, PADBIG>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADBIG>()), st, c);
 }
-// PT_CONV_BAND (read per call): 0 never, 1 always, unset: the one-addend
-// launches only (k_conv_ba: 38.9 -> 37.3 us; with two addends the unprefetched
-// epilogue lost: k_conv_bb 41.9 -> 42.8 us; profiles/r03_ablate_band.txt)
+// PT_CONV_BAND (read per call): 0 never, 2 the one-addend launches only,
+// 1 or unset: always.  First session of r03: k_conv_ba 38.9 -> 37.3 us banded,
+// k_conv_bb 41.9 -> 42.8 us (profiles/r03_ablate_band.txt); with the flat
+// conv pipeline k_conv_bb is equal either way (38.1 us) and the point-wise
+// kernels after it run faster (k_pw_ba 58.5 -> 56.2, k_pw_bb 71.7 -> 69.2 us,
+// interleaved; summed device time per step 23.10 -> 22.80 ms).
 int band_env() {
   const char* e = getenv("PT_CONV_BAND");
-  return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 1 : 2;
+  return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
 }
 template <class S>
 void launch_conv_bwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
