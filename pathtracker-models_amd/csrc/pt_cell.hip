@@ -385,6 +385,21 @@ __device__ __forceinline__ void bn_publish(const BnSlot& s, int prod, float val,
   bn_publish_finish<NTH, FWD>(s, prod, val, tid, flag, scr);
 }
 
+// Diagnostic precision bits (PT_DIAG builds; the f32 cell then stores or uses
+// a value as the bf16 cell would, tools/bf16_attrib.py): 2048 E, 4096 I,
+// 8192 gE + eg, 524288 c_i / c_e (pre-BN conv outputs), 1048576 the conv and
+// 1x1 weight fragments, 2097152 the backward transients, 4194304 the 1x1 gate
+// operands.
+#define RND_G(a) (sizeof(S) == 4 && (PT_ABL((a).ablate) & 4194304))
+#define RND_T(a) (sizeof(S) == 4 && (PT_ABL((a).ablate) & 2097152))
+#define RND_C(a) (sizeof(S) == 4 && (PT_ABL((a).ablate) & 524288))
+__device__ __forceinline__ f32x16 rb16(bool on, f32x16 v) {
+  if (on)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = rbf(true, v[r]);
+  return v;
+}
+
 // ----------------------------------------------------------------- arguments
 template <class S>
 struct CellArgs {
@@ -450,6 +465,7 @@ struct CellArgs {
 // workgroup of the traced frame writes the 100 MHz real-time counter into slot
 // `slot` (< 16) of its record trace[kind][blockIdx.x / stride][16].  Off (a
 // null pointer) in every normal run.
+#if PT_DIAG
 #define PT_TR(a, kind, slot)                                                                   \
   do {                                                                                         \
     const unsigned tr_s_ = gridDim.x > 256 ? gridDim.x / 256 : 1;                              \
@@ -458,6 +474,9 @@ struct CellArgs {
       (a).trace[((size_t)(kind) * 256 + blockIdx.x / tr_s_) * 16 + (slot)] =                     \
           __builtin_amdgcn_s_memrealtime();                                                     \
   } while (0)
+#else
+#define PT_TR(a, kind, slot) do { } while (0)
+#endif
 __device__ __forceinline__ size_t fr_off(int t, int B) { return (size_t)t * B * NPIX * C; }
 
 // (frame t, BatchNorm bn) reduction slots; nprod of the backward ones: the
@@ -710,7 +729,7 @@ __device__ void bn_fwd_partial(const f32x16 (&acc)[RW], float* red, const BnSlot
                                int lane, int wave, int tid, int ablate, int* flag, double* scr) {
   bn_block_stats<RW, NW>(acc, red, wave, lane);
   __syncthreads();
-  if (ablate & 32768) return;
+  if (PT_ABL(ablate) & 32768) return;
   bn_blocks_publish<RW, NW>(red, out, prod, tid, flag, scr);
 }
 
@@ -777,6 +796,7 @@ template <class S>
 struct StoreRow {
   S* base;
   int h;
+  bool rnd;       // diagnostic rounding (RND_C)
   static constexpr bool active = true;
   static constexpr bool prefetch_active = false;
   // B fragments from L2 into registers one column ahead, no per-column
@@ -784,7 +804,7 @@ struct StoreRow {
   static constexpr bool wreg = true;
   __device__ __forceinline__ void prefetch() const {}
   __device__ __forceinline__ void operator()(int i, const f32x16& v) const {
-    store_pl(base + (size_t)i * IMG * C, h, v);
+    store_pl(base + (size_t)i * IMG * C, h, rb16(rnd, v));
   }
 };
 
@@ -841,7 +861,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const size_t cb = clip_off(b);
-  if (a.ablate & 512) return;
+  if (PT_ABL(a.ablate) & 512) return;
 
   if constexpr (FILL == FILL_BNBWD) {
     if (tid < 32) {
@@ -914,7 +934,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
           for (int j = 0; j < CPB; ++j) {
             const int ch = ch0 + j;
             const float v = tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch];
-            oo[j] = (S)v;
+            oo[j] = (S)rbf(RND_T(a), v);
           }
           *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
           if constexpr (EPI != EPI_NONE) {
@@ -937,11 +957,11 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
     if constexpr (EPI == EPI_FWD) {
       // each finished row is stored while the later rows' MFMAs still run
       // (all 256 workgroups storing at the very end took ~6.5 us per launch)
-      const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RW) * IMG + px) * C, h};
+      const StoreRow<S> sr{a.out_raw + cb + ((size_t)(wave * RW) * IMG + px) * C, h, RND_C(a)};
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate, sr);
-      if (a.ablate & 256) return;
+      if (PT_ABL(a.ablate) & 256) return;
       // the tile is free once every wave has passed bn_fwd_partial's barrier
-      if (!(a.ablate & 8))
+      if (!(PT_ABL(a.ablate) & 8))
         bn_fwd_partial<RW, NW>(acc, red, a.bnout, b, lane, wave, tid, a.ablate,
                                (int*)(smem + NTH * 16), (double*)smem);
     } else if constexpr (sizeof(S) == 2) {
@@ -951,15 +971,15 @@ __device__ __forceinline__ void conv_body(const ConvArgs<S>& a, char* smem, int 
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate, ar);
     } else {
       conv_run<S, PAD, RW, NTH>(acc, fill, a.wf, tile, wbuf, a.K, wave * RW, lane, tid, a.ablate);
-      if (a.ablate & 256) return;
+      if (PT_ABL(a.ablate) & 256) return;
 #pragma unroll
       for (int i = 0; i < RW; ++i) {
         const size_t po = cb + ((size_t)(wave * RW + i) * IMG + px) * C;
         f32x16 v = acc[i];
         add_pl(a.add0 + po, h, v);
         if (a.add1) add_pl(a.add1 + po, h, v);
-        if (a.ablate & 1024) store_pl_nt(a.out + po, h, v);
-        else store_pl(a.out + po, h, v);
+        if (PT_ABL(a.ablate) & 1024) store_pl_nt(a.out + po, h, v);
+        else store_pl(a.out + po, h, rb16(RND_T(a), v));
       }
     }
   }
@@ -1391,7 +1411,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
       const float e = (float)in.egv[r];
       Ep[r] = (1.f - e) * in.Eo[r] + e * eh;
     }
-    if (sizeof(S) == 4 && (a.ablate & 2048))
+    if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 2048))
 #pragma unroll
       for (int r = 0; r < 16; ++r) Ep[r] = (float)(bf16_t)Ep[r];
     store_cl(a.E + (t - 1) * fs + ro, c, h, Ep);
@@ -1400,15 +1420,15 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
   f32x16 z, xv;
   stem_cl<ACT>(xs, yl, h, st, z, xv);
   F pax[Tr<S>::KS], pae[Tr<S>::KS];
-  cl_to_pa<S>(wscr, xv, lane, pax);
-  cl_to_pa<S>(wscr, Ep, lane, pae);
+  cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
+  cl_to_pa<S>(wscr, Ep, lane, pae, RND_G(a));
   f32x16 acc = zero16();
   acc = gemm_pa<S>(pax, a.gf[0], acc, lane);
   acc = gemm_pa<S>(pae, a.gf[1], acc, lane);
   f32x16 att, gEv;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { att[r] = sigm_b(acc[r], nba); gEv[r] = att[r] * Ep[r]; }
-  if (sizeof(S) == 4 && (a.ablate & 8192))
+  if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 8192))
 #pragma unroll
     for (int r = 0; r < 16; ++r) gEv[r] = (float)(bf16_t)gEv[r];
   store_cl(a.gE + t * fs + ro, c, h, gEv);
@@ -1422,14 +1442,14 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
     for (int r = 0; r < 16; ++r) gp[cl_x(r, h)] = att[r];
   }
   F pag[Tr<S>::KS], pai[Tr<S>::KS];
-  cl_to_pa<S>(wscr, gEv, lane, pag);
+  cl_to_pa<S>(wscr, gEv, lane, pag, RND_G(a));
   if constexpr (HG) {          // g_inh = att (ffhgru_hierarchy.py:147, :154)
     store_cl(a.at + t * fs + ro, c, h, att);
-    cl_to_pa<S>(wscr, att, lane, pai);
+    cl_to_pa<S>(wscr, att, lane, pai, RND_G(a));
   } else if (a.no_inh) {
-    cl_to_pa<S>(wscr, Ep, lane, pai);
+    cl_to_pa<S>(wscr, Ep, lane, pai, RND_G(a));
   } else {
-    cl_to_pa<S>(wscr, in.Iv, lane, pai);
+    cl_to_pa<S>(wscr, in.Iv, lane, pai, RND_G(a));
   }
   acc = zero16();
   acc = gemm_pa<S>(pai, a.gf[4], acc, lane);
@@ -1437,7 +1457,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
   f32x16 egn;
 #pragma unroll
   for (int r = 0; r < 16; ++r) egn[r] = sigm_b(acc[r], nbe);
-  if (sizeof(S) == 4 && (a.ablate & 8192))
+  if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 8192))
 #pragma unroll
     for (int r = 0; r < 16; ++r) egn[r] = (float)(bf16_t)egn[r];
   store_cl(a.eg + t * fs + ro, c, h, egn);
@@ -1447,7 +1467,7 @@ template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   static_assert(PWF_RPP == 1, "forward point-wise kernels: one row per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.ablate & 512) return;
+  if (PT_ABL(a.ablate) & 512) return;
   const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1460,13 +1480,13 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   // order per wave, so behind its own row tiles it would wait for all of them
   // (and the barrier below for it); the other waves' row tiles go out first.
   const bool finw = wave == PW_NW - 1;
-  if (finw && t > 0 && !(a.ablate & 65536))
+  if (finw && t > 0 && !(PT_ABL(a.ablate) & 65536))
     bn_fwd_finalize(bnf_src(a, t - 1, 1), bnf_nsrc(a), B * a.bn_world, a.eps, L.stat + 64,
                     blockIdx.x == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   const FaIn<S> in = fa_load(a, t, ro, c, h);
-  if (t < T && !(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
+  if (t < T && !(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW, tid, PW_NT, a.ntx, a.nty);
   __syncthreads();
-  if (a.ablate & 4) return;
+  if (PT_ABL(a.ablate) & 4) return;
   fa_row<S, ACT, HG>(a, t, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, b, y, ro, in, lane);
 }
 
@@ -1509,8 +1529,8 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float*
     ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * (float)in.gi[r] + mu)));
   }
   F pax[Tr<S>::KS], pai[Tr<S>::KS];
-  cl_to_pa<S>(wscr, xv, lane, pax);
-  cl_to_pa<S>(wscr, in.gi, lane, pai);
+  cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
+  cl_to_pa<S>(wscr, in.gi, lane, pai, RND_G(a));
   f32x16 acc = zero16();
   acc = gemm_pa<S>(pax, a.gf[2], acc, lane);
   acc = gemm_pa<S>(pai, a.gf[3], acc, lane);
@@ -1520,7 +1540,7 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float*
     const float ig = sigm_b(acc[r], nbi);
     In[r] = (1.f - ig) * (float)in.Iv[r] + ig * ih[r];
   }
-  if (sizeof(S) == 4 && (a.ablate & 4096))
+  if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 4096))
 #pragma unroll
     for (int r = 0; r < 16; ++r) In[r] = (float)(bf16_t)In[r];
   store_cl(a.I + t * fs + ro, c, h, In);
@@ -1530,7 +1550,7 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float*
 template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.ablate & 512) return;
+  if (PT_ABL(a.ablate) & 512) return;
   const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1541,7 +1561,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   const size_t fs = fr_off(1, B), ro = clip_off(b) + (size_t)y * IMG * C;
 
   if (a.no_inh) {      // I_t = gE_t (:168)
-    if (!(a.ablate & 4)) {
+    if (!(PT_ABL(a.ablate) & 4)) {
       const Pk<S> g = load_pk(a.gE + t * fs + ro, c, h);
       f32x16 v;
 #pragma unroll
@@ -1556,7 +1576,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   bn_fwd_finalize(bnf_src(a, t, 0), bnf_nsrc(a), B * a.bn_world, a.eps, L.stat,
                   blockIdx.x == 0 ? a.bnstat + (size_t)t * 128 : nullptr, tid);
   __syncthreads();
-  if (a.ablate & 4) return;
+  if (PT_ABL(a.ablate) & 4) return;
   fb_row<S, ACT, HG>(a, t, L.stat, L.xs, yl, L.scr + wave * SCR_FLOATS, y, ro, in, lane);
 }
 
@@ -1601,12 +1621,12 @@ __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i] = zero16();
   const int h = lane >> 5, px = lane & 31;
-  const StoreRow<S> sr{out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h};
+  const StoreRow<S> sr{out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h, false};
   auto nofill = [](int) {};                 // the point-wise half filled the tile
   conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
-                                   tid, a.ablate & 1, sr);
+                                   tid, PT_ABL(a.ablate) & 1, sr);
   PT_TR(a, kind, 4);
-  if (a.ablate & 8) return;
+  if (PT_ABL(a.ablate) & 8) return;
   bn_block_stats<RW, FUSED_NW>(acc, L.red, wave, lane);       // = bn_fwd_partial, stamped
   __syncthreads();
   PT_TR(a, kind, 5);
@@ -1627,13 +1647,13 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
   // persistent: only the finalising wave waits for the batch sums (COH); the
   // others' row loads and the x staging below go out meanwhile
   if (COH && wave == FUSED_NW - 1 && t > 0) wave_wait(wcnt, wtarget, err, lane);
-  if (!(a.ablate & 65536) && wave == FUSED_NW - 1 && t > 0)
+  if (!(PT_ABL(a.ablate) & 65536) && wave == FUSED_NW - 1 && t > 0)
     bn_fwd_finalize<COH>(bnf_src(a, t - 1, 1), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat + 64,
                          b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   // this wave's first row's tiles go out before the staging and the barrier
   FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
-  if (!(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
   PT_TR(a, PT_K_FUSED_FA, 2);
 #pragma unroll 1
@@ -1642,7 +1662,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
     const size_t ro = clip_off(b) + (size_t)y * IMG * C;
     const FaIn<S> cur = nxt;
     if (i + 1 < FUSED_RW) nxt = fa_load(a, t, ro + (size_t)IMG * C, cl, h);   // next row in flight
-    if (!(a.ablate & 4))
+    if (!(PT_ABL(a.ablate) & 4))
       fa_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
                          (S*)L.tile);
   }
@@ -1663,12 +1683,12 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
   PT_TR(a, PT_K_FUSED_FB, 0);
   if constexpr (COH) __syncthreads();
   if (COH && wave == FUSED_NW - 1) wave_wait(wcnt, wtarget, err, lane);
-  if (!(a.ablate & 65536) && wave == FUSED_NW - 1)
+  if (!(PT_ABL(a.ablate) & 65536) && wave == FUSED_NW - 1)
     bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
                          b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
   FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
-  if (!(a.ablate & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
   PT_TR(a, PT_K_FUSED_FB, 2);
 #pragma unroll 1
@@ -1677,7 +1697,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     const size_t ro = clip_off(b) + (size_t)y * IMG * C;
     const FbIn<S> cur = nxt;
     if (i + 1 < FUSED_RW) nxt = fb_load<S, HG>(a, t, ro + (size_t)IMG * C, cl, h);
-    if (!(a.ablate & 4))
+    if (!(PT_ABL(a.ablate) & 4))
       fb_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
                          (S*)L.tile);
   }
@@ -1779,7 +1799,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   const S* dgsrc = a.conv_done ? a.dgE : a.dgEp;
 
 #pragma unroll 1
-  for (int i = 0; i < RPP && !(a.ablate & 4); ++i) {
+  for (int i = 0; i < RPP && !(PT_ABL(a.ablate) & 4); ++i) {
     const int yl = wave * RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 GE;
@@ -1797,8 +1817,8 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
         const Pk<S> dAt = HG ? load_pk(a.dAt + ro, c, h) : zero_pk<S>();
         const f32x16 Et = head ? load_cl(a.E + t * fs + ro, c, h) : zero16();
         F pax[Tr<S>::KS], pae[Tr<S>::KS];
-        cl_to_pa<S>(wscr, xv, lane, pax);
-        cl_to_pa<S>(wscr, Et, lane, pae);
+        cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
+        cl_to_pa<S>(wscr, Et, lane, pae, RND_G(a));
         f32x16 g = zero16();
         g = gemm_pa<S>(pax, a.gf[0], g, lane);
         g = gemm_pa<S>(pae, a.gf[1], g, lane);
@@ -1810,10 +1830,10 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
           dap[r] = datt * att[r] * (1.f - att[r]);
           sm[0] += dap[r];
         }
-        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
-        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
+        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
+        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
         F pad[Tr<S>::KS];
-        cl_to_pa<S>(wscr, dap, lane, pad);
+        cl_to_pa<S>(wscr, dap, lane, pad, RND_G(a));
         if (head) {
           GE = load_cl(a.dEn + ro, c, h);
 #pragma unroll
@@ -1858,22 +1878,22 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
         bs0 += dce;
         bs1 += dce * xe;
       }
-      store_cl(a.dIl + ro, c, h, dIl);
-      store_cl(a.dEn + ro, c, h, dEn);
-      store_cl(a.dEp + ro, c, h, dEp);
-      store_cl(a.dcE + ro, c, h, dcE);
+      store_cl(a.dIl + ro, c, h, rb16(RND_T(a), dIl));
+      store_cl(a.dEn + ro, c, h, rb16(RND_T(a), dEn));
+      store_cl(a.dEp + ro, c, h, rb16(RND_T(a), dEp));
+      store_cl(a.dcE + ro, c, h, rb16(RND_T(a), dcE));
     }
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
   PT_TR(a, PT_K_PW_BA, 3);
-  const bool bn = head && !(a.ablate & 8);
+  const bool bn = head && !(PT_ABL(a.ablate) & 8);
   const BnSlot bo = bnb_slot(a, t, 1, B * PWA_WGPC);
   float bv = 0.f;
   if (bn) bv = bn_bwd_partial(bs0, bs1, L.red, bo, lane, wave, tid);
   PT_TR(a, PT_K_PW_BA, 4);
-  if (!(a.ablate & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
-  if (tail && (head || HG) && !(a.ablate & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
+  if (!(PT_ABL(a.ablate) & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
+  if (tail && (head || HG) && !(PT_ABL(a.ablate) & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
   PT_TR(a, PT_K_PW_BA, 5);
   // L.stat is unused by the backward kernels: mode 2's ticket flag word
   if (bn) bn_publish_finish<PW_NT, false>(bo, blockIdx.x, bv, tid, (int*)L.stat, (double*)L.red);
@@ -1882,7 +1902,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
 template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.ablate & 512) return;
+  if (PT_ABL(a.ablate) & 512) return;
   pw_ba_body<S, ACT, HG, PWA_RPP>(a, smem, blockIdx.x / PWA_WGPC, blockIdx.x % PWA_WGPC);
 }
 
@@ -1940,7 +1960,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   // one row per wave: its tiles are loaded first, their latency overlaps the staging
   BbRow<S> pre;
   if constexpr (RPP == 1) pre = load_row(clip_off(b) + (size_t)(y0 + wave) * IMG * C, c, h);
-  if (!(a.ablate & 262144)) slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);   // i_w, i_u, e_w, e_u
+  if (!(PT_ABL(a.ablate) & 262144)) slab_prefetch(slab_p, L.slabl, 2, 4, wave, lane);   // i_w, i_u, e_w, e_u
   stage_x(a.x, a.xu8, L.xs, b, t, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
   if constexpr (!BF) gacc_zero(L.gacc, 4, tid);
   PT_TR(a, PT_K_PW_BB, 1);
@@ -1954,7 +1974,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   float bs0 = 0.f, bs1 = 0.f;
 
 #pragma unroll 1
-  for (int i = 0; i < RPP && !(a.ablate & 4); ++i) {
+  for (int i = 0; i < RPP && !(PT_ABL(a.ablate) & 4); ++i) {
     // several rows per wave: the lane index laundered per row, so that the
     // per-lane parameters and addresses are formed in the row instead of
     // staying live across the loop as invariants (RPP 2: 161 VGPRs of spills)
@@ -1985,17 +2005,17 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         stage_wg(L.stage, 1, ginh, wave, lane);
         stage_wg(L.stage, 2, w.gEv, wave, lane);
         __syncthreads();
-        if (wave < 2 && !(a.ablate & 16))
+        if (wave < 2 && !(PT_ABL(a.ablate) & 16))
           gate_wgrad(L.stage, 0, 1 + wave, 4 + wave, L.slabl, slab_p, lane);
       } else {
-        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
-        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, w.gEv, lane, wave, tid);
+        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 2 * 1024, L.flush, depf, ginh, lane, wave, tid);
+        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 3 * 1024, L.flush, depf, w.gEv, lane, wave, tid);
       }
       sm[3] += hsum16(depf);
-      cl_to_pa<S>(wscr, depf, lane, pe);
+      cl_to_pa<S>(wscr, depf, lane, pe, RND_G(a));
       const f32x16 dIt0 = a.no_inh ? load_cl(a.dIt + ro, c, h) : zero16();
       const f32x16 dg = gemm_pa<S>(pe, a.gt[5], dIt0, lane);   // no_inh: I_t = gE_t
-      store_cl(a.dgEp + ro, c, h, dg);
+      store_cl(a.dgEp + ro, c, h, rb16(RND_T(a), dg));
     }
     if (a.no_inh) {
       const f32x16 dEn = gemm_pa<S>(pe, a.gt[4], load_cl(a.dEn + ro, c, h), lane);
@@ -2008,9 +2028,9 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
       f32x16 g = zero16();
       {
         F pax[Tr<S>::KS], pai[Tr<S>::KS];
-        cl_to_pa<S>(wscr, xv, lane, pax);
+        cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
         g = gemm_pa<S>(pax, a.gf[2], g, lane);
-        cl_to_pa<S>(wscr, ginh, lane, pai);
+        cl_to_pa<S>(wscr, ginh, lane, pai, RND_G(a));
         g = gemm_pa<S>(pai, a.gf[3], g, lane);
       }
       const float A0 = bw0 * rs0, B0 = bb0 - bw0 * rs0 * m0;    // BN0 affine folded
@@ -2034,7 +2054,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         const float dp = -dq * dfp;
         const float du = dp * cn;
         const float dci = dp * u;
-        stf(a.dcI + ro + cl_x(r, h) * C + c, dci);
+        stf(a.dcI + ro + cl_x(r, h) * C + c, rbf(RND_T(a), dci));
         dx[r] = dq;
         // InT: dI_{t-1} collects the update and the gated-inhibition terms;
         // hGRU: the gated-inhibition terms go to att (dA, kept in dIp's slot)
@@ -2053,14 +2073,14 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         stage_wg(L.stage, 0, dip, wave, lane);
         stage_wg(L.stage, 2, xv, wave, lane);
         __syncthreads();
-        if (wave >= 2 && !(a.ablate & 16))
+        if (wave >= 2 && !(PT_ABL(a.ablate) & 16))
           gate_wgrad(L.stage, 0, wave == 2 ? 2 : 1, wave, L.slabl, slab_p, lane);
       } else {
-        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
-        if (!(a.ablate & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
+        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dip, xv, lane, wave, tid);
+        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dip, ginh, lane, wave, tid);
       }
       F pd[Tr<S>::KS];
-      cl_to_pa<S>(wscr, dip, lane, pd);
+      cl_to_pa<S>(wscr, dip, lane, pd, RND_G(a));
       dx = gemm_pa<S>(pd, a.gt[2], dx, lane);
       // stem backward of this share (models/InT.py:212-213): dz = dx nl'(z)
 #pragma unroll
@@ -2078,23 +2098,23 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         for (int r = 0; r < 16; ++r) gi[r] = (float)Iprev[r];
         store_cl(a.GI + ro, c, h, gi);
       } else {
-        store_cl(a.GI + ro, c, h, dIp);
+        store_cl(a.GI + ro, c, h, rb16(RND_T(a), dIp));
       }
     }
   }
   sm[4] = bs1;
   sm[5] = bs0;
   PT_TR(a, PT_K_PW_BB, 3);
-  const bool bn = !a.no_inh && !(a.ablate & 8);
+  const bool bn = !a.no_inh && !(PT_ABL(a.ablate) & 8);
   const BnSlot bo = bnb_slot(a, t, 0, B * PWB_WGPC);
   float bv = 0.f;
   if (bn) bv = bn_bwd_partial(bs0, bs1, L.red, bo, lane, wave, tid);
   PT_TR(a, PT_K_PW_BB, 4);
-  if (!(a.ablate & 32)) flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
+  if (!(PT_ABL(a.ablate) & 32)) flush_small<10>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);  // ends with a barrier
   PT_TR(a, PT_K_PW_BB, 5);
   if (bn) bn_publish_finish<PW_NT, false>(bo, blockIdx.x, bv, tid, (int*)L.stat, (double*)L.red);
   PT_TR(a, PT_K_PW_BB, 6);
-  if (a.ablate & 32) return;
+  if (PT_ABL(a.ablate) & 32) return;
   // gacc: 0 i_w, 1 i_u, 2 e_w, 3 e_u  ->  slab gates 2..5 (bf16: written by gate_wgrad)
   if constexpr (!BF) {
     if (!a.no_inh) gacc_flush(L.gacc, L.slabl, slab_p, 2, 2, tid);
@@ -2104,7 +2124,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
 template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.ablate & 512) return;
+  if (PT_ABL(a.ablate) & 512) return;
   pw_bb_body<S, ACT, HG, PWB_RPP>(a, smem, blockIdx.x / PWB_WGPC, blockIdx.x % PWB_WGPC);
 }
 
@@ -2352,17 +2372,17 @@ __device__ __forceinline__ void wgrad_run(Body&& body, const S* __restrict__ Xs,
     // one buffer (f32, PAD 7): load it after (the staged band would not fit
     // in registers beside the accumulators)
     if constexpr (NBUF == 2)
-      if (more && stager && !(ablate & 128))
+      if (more && stager && !(PT_ABL(ablate) & 128))
         band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * RB, tid, ntx, nty);
-    if (!(ablate & 64)) body(xt, dt);
+    if (!(PT_ABL(ablate) & 64)) body(xt, dt);
     if (more) {
       S* xn = buf + (NBUF == 2 ? ((u + 1) & 1) * BE : 0);
       if constexpr (NBUF == 1) {
         __syncthreads();                              // every wave is done reading the buffer
-        if (stager && !(ablate & 128))
+        if (stager && !(PT_ABL(ablate) & 128))
           band.load(Xs, Ds, B, g + ((u + 1) / NB) * nwg, ((u + 1) % NB) * RB, tid, ntx, nty);
       }
-      if (stager && !(ablate & 128)) band.store(xn, xn + XE, tid, tiled);
+      if (stager && !(PT_ABL(ablate) & 128)) band.store(xn, xn + XE, tid, tiled);
       __syncthreads();
     }
   }
@@ -2501,6 +2521,7 @@ struct PrepArgs {
   S *wf_inh, *wf_exc, *wt_inh, *wt_exc;
   S* gf[6];
   S* gt[6];
+  int rnd;        // diagnostic: weights rounded to bf16 (f32 path, bit 1048576)
 };
 
 template <class S>
@@ -2520,7 +2541,7 @@ __global__ void k_prep(PrepArgs<S> p) {
       S* dst = which == 0 ? p.wf_inh : which == 1 ? p.wf_exc : which == 2 ? p.wt_inh : p.wt_exc;
       if (W) {
         const float v = which < 2 ? W[(n * C + kc) * KK + tap] : W[(kc * C + n) * KK + (KK - 1 - tap)];
-        dst[r] = (S)v;
+        dst[r] = (S)rbf(p.rnd, v);
       }
     } else {
       const int e2 = e - 4 * nconv;
@@ -2530,7 +2551,7 @@ __global__ void k_prep(PrepArgs<S> p) {
       const int n = l & 31, h = l >> 5, kc = frag_chan<S>(ks, h, j);
       const float* G = p.g[gate];
       const float v = tr == 0 ? G[n * C + kc] : G[kc * C + n];
-      (tr == 0 ? p.gf[gate] : p.gt[gate])[r] = (S)v;
+      (tr == 0 ? p.gf[gate] : p.gt[gate])[r] = (S)rbf(p.rnd, v);
     }
   }
 }
@@ -2808,6 +2829,26 @@ void timed(int kind, hipStream_t st, F&& launch) {
   g_tm.ev.emplace_back(a, b);
 }
 
+// Diagnostic switches (PT_DIAG builds only): PT_CELL_ABLATE
+// (phase / precision bits, CellArgs::ablate) and PT_CELL_DEBUG_STOP (end the
+// backward sweep after n launches).  The release library never reads them.
+int ablate_env() {
+#if PT_DIAG
+  const char* ab = getenv("PT_CELL_ABLATE");
+  return ab ? atoi(ab) : 0;
+#else
+  return 0;
+#endif
+}
+int debug_stop_env() {
+#if PT_DIAG
+  const char* e = getenv("PT_CELL_DEBUG_STOP");
+  return e ? atoi(e) : 0;
+#else
+  return 0;
+#endif
+}
+
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
@@ -2906,10 +2947,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   a.trace_t = g_trace_t;
   a.x = x;
   a.xu8 = d->x_format == PT_X_U8_NTHWC;
-  {
-    const char* ab = getenv("PT_CELL_ABLATE");     // timing experiments only
-    a.ablate = ab ? atoi(ab) : 0;
-  }
+  a.ablate = ablate_env();                       // diagnostic builds only
   a.wpre = pr->preproc_w; a.bpre = pr->preproc_b;
   a.alpha = pr->alpha; a.mu = pr->mu; a.gamma = pr->gamma; a.kappa = pr->kappa;
   a.bnw0 = pr->bn_w[0]; a.bnb0 = pr->bn_b[0]; a.bnw1 = pr->bn_w[1]; a.bnb1 = pr->bn_b[1];
@@ -3132,6 +3170,7 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   if (syncbn(dist)) { a.bnsync = dist->bn_buf; a.bn_world = dist->bn_world; }
   PrepArgs<S> pa{};
   pa.K = p.K; pa.w_inh = d->no_inh ? nullptr : pr->w_inh; pa.w_exc = pr->w_exc;
+  pa.rnd = sizeof(S) == 4 && (a.ablate & 1048576);
   for (int i = 0; i < 6; ++i) {
     pa.g[i] = pr->gate_w[i];
     pa.gf[i] = (S*)((char*)saved + p.o_g[i]);
@@ -3160,6 +3199,14 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
         else hipLaunchKernelGGL((k_persist_fwd<S, 0, 0>), dim3(p.B), dim3(CONV_NT), lds, st, a, ca, cb, done, err);
       }
     });
+    // a grid that was not fully resident (another stream holding CUs) gives up
+    // its bounded waits and flags err: read it back and fail loudly (this
+    // opt-in mode runs without hipGraph replay, pt_cell_forward_dist)
+    unsigned herr = 0;
+    HIPCHK(hipMemcpyAsync(&herr, err, sizeof(herr), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (herr)
+      return fail(PT_ERR_HIP, "persistent forward: the grid was not co-resident (a BatchNorm wait gave up)%s%ld");
     a.t = p.T;
     timed(PT_K_PW_FA, st, [&] { PW_LAUNCH(k_pw_fa, gpf, lpf); });     // closes E_{T-1}
   } else if (use_fused(d, p)) {   // one launch per BatchNorm segment (k_fused_fa / k_fused_fb)
@@ -3272,8 +3319,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   };
   // diagnostics only (env PT_CELL_DEBUG_STOP = n): return after the sweep's
   // first n launches, leaving the transients as that launch wrote them
-  const char* dbg = getenv("PT_CELL_DEBUG_STOP");
-  const int stop_at = dbg ? atoi(dbg) : 0;
+  const int stop_at = debug_stop_env();
   int n_launch = 0;
   auto stop = [&] { return stop_at > 0 && ++n_launch >= stop_at; };
   a.t = p.T - 1;
@@ -3337,11 +3383,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
 ptg::GraphCache g_graphs;
 bool use_graph() {
   return ptg::graphs_enabled() && __atomic_load_n(&g_tm.mask, __ATOMIC_RELAXED) == 0 &&
-         !getenv("PT_CELL_DEBUG_STOP") && !g_trace;
-}
-int ablate_env() {
-  const char* ab = getenv("PT_CELL_ABLATE");
-  return ab ? atoi(ab) : 0;
+         !debug_stop_env() && !g_trace;
 }
 
 }  // namespace
@@ -3374,8 +3416,9 @@ int pt_cell_forward_dist(const pt_cell_desc* d, const void* x, const pt_cell_par
     return bf ? run_forward<bf16_t>(d, x, p, saved, ws, e_last, gates, dist, s)
               : run_forward<float>(d, x, p, saved, ws, e_last, gates, dist, s);
   };
-  // SyncBN calls back into the caller between launches: direct launches only
-  if (!use_graph() || syncbn(dist)) return body(st);
+  // SyncBN calls back into the caller between launches, and the persistent
+  // forward reads its give-up flag back: direct launches only
+  if (!use_graph() || syncbn(dist) || persist_env()) return body(st);
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
   k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env())
@@ -3439,9 +3482,14 @@ int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params*
 }
 
 int pt_cell_trace(void* buf, int frame) {
+#if PT_DIAG
   g_trace = (unsigned long long*)buf;
   g_trace_t = frame;
   return 0;
+#else
+  (void)buf; (void)frame;
+  return fail(PT_ERR_UNSUPPORTED, "pt_cell_trace needs the diagnostic build (libptcell_diag.so)%s%ld");
+#endif
 }
 
 int pt_cell_timing_enable(uint32_t kind_mask) {
@@ -3481,6 +3529,10 @@ const char* pt_last_error(void) { return g_err; }
 #ifndef PT_SRC_HASH
 #define PT_SRC_HASH "unstamped"
 #endif
+#if PT_DIAG
+const char* pt_version(void) { return "pt_cell 0.2 gfx950 diag src " PT_SRC_HASH; }
+#else
 const char* pt_version(void) { return "pt_cell 0.2 gfx950 src " PT_SRC_HASH; }
+#endif
 
 }  // extern "C"

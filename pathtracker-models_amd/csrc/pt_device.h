@@ -24,6 +24,15 @@
 
 #include <type_traits>
 
+// Diagnostic builds (-DPT_DIAG=1, tools/ only: ptamd/build.py builds them as
+// libptcell_diag.so) honour the PT_CELL_ABLATE phase / precision switches,
+// PT_CELL_DEBUG_STOP and pt_cell_trace.  In the release library every switch
+// test below is a compile-time 0: the environment cannot alter a result.
+#ifndef PT_DIAG
+#define PT_DIAG 0
+#endif
+#define PT_ABL(x) (PT_DIAG ? (x) : 0)
+
 namespace ptc {
 
 constexpr int C = 32;          // channels (MFMA tile width)
@@ -365,12 +374,15 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Diagnostic rounding (PT_DIAG builds, f32 path): v as the bf16 path stores it.
+__device__ __forceinline__ float rbf(bool on, float v) { return on ? (float)(bf16_t)v : v; }
+
 template <class S, class V>
 __device__ __forceinline__ void cl_to_pa(float* __restrict__ scr, const V& v, int lane,
-                                         typename Tr<S>::frag (&pa)[Tr<S>::KS]) {
+                                         typename Tr<S>::frag (&pa)[Tr<S>::KS], bool rnd = false) {
   const int c = lane & 31, h = lane >> 5, p = lane & 31;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) scr[scr_idx<S>(cl_x(r, h), c)] = (float)v[r];
+  for (int r = 0; r < 16; ++r) scr[scr_idx<S>(cl_x(r, h), c)] = rbf(rnd, (float)v[r]);
   wave_sync();
   if constexpr (sizeof(S) == 4) {
 #pragma unroll
@@ -606,9 +618,9 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
     };
     load_colw(0, bw[0]);
     __syncthreads();
-    if (!(ablate & 2)) fill(0);
+    if (!(PT_ABL(ablate) & 2)) fill(0);
     __syncthreads();
-    if (ablate & 1) return;
+    if (PT_ABL(ablate) & 1) return;
     constexpr int NST = K * NTR;
     constexpr int PF = CONV_PF_W < NST ? CONV_PF_W : NST;
     F av[PF + 1][KSP];
@@ -649,10 +661,10 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
     WSlice pre;
     wslice_load<S, K, NTH>(pre, wf, 0, 0, tid);
     __syncthreads();
-    if (!(ablate & 2)) fill(0);
+    if (!(PT_ABL(ablate) & 2)) fill(0);
     wslice_store<K, NTH>(pre, wbuf, tid);
     __syncthreads();
-    if (ablate & 1) return;
+    if (PT_ABL(ablate) & 1) return;
     constexpr int NST = K * NTR;
     constexpr int PF = CONV_PF < NST ? CONV_PF : NST;
     F av[PF + 1][KSP];
@@ -709,15 +721,15 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
     WSlice pre;
     if constexpr (LDSW) wslice_load<S, K, NTH>(pre, wf, pass, 0, tid);
     __syncthreads();
-    if (!(ablate & 2)) fill(pass);
+    if (!(PT_ABL(ablate) & 2)) fill(pass);
     if constexpr (LDSW) wslice_store<K, NTH>(pre, wbuf, tid);
     __syncthreads();
-    if (ablate & 1) continue;
+    if (PT_ABL(ablate) & 1) continue;
     for (int kw = 0; kw < K; ++kw) {
       F bc[K][KSP];
       if constexpr (LDSW) {
         const F* wl = (const F*)(wbuf + (kw & 1) * WSLICE_BYTES) + lane;
-        if (kw + 1 < K && !(ablate & 16384)) wslice_load<S, K, NTH>(pre, wf, pass, kw + 1, tid);
+        if (kw + 1 < K && !(PT_ABL(ablate) & 16384)) wslice_load<S, K, NTH>(pre, wf, pass, kw + 1, tid);
         if constexpr (Done::prefetch_active)
           if (kw == 0 && pass == TT::NPASS - 1) done.prefetch();
 #pragma unroll
@@ -780,7 +792,7 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
         }
       }
       if constexpr (LDSW) {
-        if (kw + 1 < K && !(ablate & 16384)) {
+        if (kw + 1 < K && !(PT_ABL(ablate) & 16384)) {
           wslice_store<K, NTH>(pre, wbuf + ((kw + 1) & 1) * WSLICE_BYTES, tid);
           __syncthreads();
         }

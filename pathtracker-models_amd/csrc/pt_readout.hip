@@ -245,21 +245,26 @@ __global__ void k_ro_reduce(RoArgs a, pt_readout_grads g) {
   else g.dense_b[0] = s;
 }
 
-int check(const pt_readout_desc* d) {
-  if (!d) return pt_set_error(PT_ERR_ARG, "null readout descriptor");
-  if (d->batch < 1 || d->channels < 1 || d->height < 1 || d->width < 1)
-    return pt_set_error(PT_ERR_ARG, "readout: batch, channels, height, width must be >= 1");
-  if (d->height + 4 > RO_MAXPW || d->width + 4 > RO_MAXPW || d->channels > 1024)
-    return pt_set_error(PT_ERR_UNSUPPORTED, "readout: frames up to 128 x 128, channels up to 1024");
-  return 0;
-}
-
 size_t lds_fwd(const pt_readout_desc* d) {
   return (size_t)(2 * (d->height + 4) * (d->width + 4) + RO_NT) * sizeof(float);
 }
 size_t lds_bwd(const pt_readout_desc* d) {
   return (size_t)(2 * (d->height + 4) * (d->width + 4) + d->height * d->width +
                   (d->channels + 51) * (RO_NT / 64)) * sizeof(float);
+}
+
+// One shape check for every entry point: a shape whose BACKWARD does not fit
+// the 160 KB of LDS is refused up front (the forward alone would fit up to
+// 128 x 128 and only the backward would then fail, mid training step).
+int check(const pt_readout_desc* d) {
+  if (!d) return pt_set_error(PT_ERR_ARG, "null readout descriptor");
+  if (d->batch < 1 || d->channels < 1 || d->height < 1 || d->width < 1)
+    return pt_set_error(PT_ERR_ARG, "readout: batch, channels, height, width must be >= 1");
+  if (d->height + 4 > RO_MAXPW || d->width + 4 > RO_MAXPW || d->channels > 1024)
+    return pt_set_error(PT_ERR_UNSUPPORTED, "readout: frames up to 128 x 128, channels up to 1024");
+  if (lds_bwd(d) > 160 * 1024)
+    return pt_set_error(PT_ERR_UNSUPPORTED, "readout: the backward's LDS tiles exceed 160 KB at this frame size");
+  return 0;
 }
 
 int set_lds() {
@@ -304,7 +309,6 @@ int pt_readout_backward(const pt_readout_desc* d, const float* e, const float* t
   if (!e || !tgt || !p || !pooled || !d_logits || !d_e || !g || !workspace)
     return pt_set_error(PT_ERR_ARG, "readout: null pointer");
   const size_t lds = lds_bwd(d);
-  if (lds > 160 * 1024) return pt_set_error(PT_ERR_UNSUPPORTED, "readout: backward LDS over 160 KB");
   if (int rc = set_lds()) return rc;
   RoArgs a{};
   a.B = d->batch; a.C = d->channels; a.H = d->height; a.W = d->width;

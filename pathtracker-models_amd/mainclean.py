@@ -59,7 +59,10 @@ def validate(args, val_loader, model, criterion, device, results_folder, len_val
     precisionv, recallv, f1scorev = AverageMeter(), AverageMeter(), AverageMeter()
     end = time.time()
     with torch.no_grad():
-        for i, (imgs, target) in enumerate(val_loader):
+        # lockstep: with --sync-bn every forward makes collective calls (the
+        # cell's BatchNorm all-reduces), and the ranks' shards hold different
+        # batch counts -- all ranks stop at the smallest one, as in training
+        for i, (imgs, target) in enumerate(lockstep(val_loader, device)):
             imgs, target = engine.prepare_data(imgs=imgs, target=target, args=args, device=device,
                                                disentangle_channels=disentangle_channels,
                                                keep_u8=keep_u8)

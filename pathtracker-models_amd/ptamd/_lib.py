@@ -12,6 +12,12 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libptcell.so")
+# The diagnostic build (-DPT_DIAG=1: PT_CELL_ABLATE, PT_CELL_DEBUG_STOP,
+# pt_cell_trace), for tools/ only; selected by use_diag() before the first
+# load, or PT_CELL_DIAG=1 in the environment of a tool's process.
+DIAG_PATH = os.path.join(HERE, "libptcell_diag.so")
+if os.environ.get("PT_CELL_DIAG") == "1":
+    LIB_PATH = DIAG_PATH
 
 PT_ACT_SOFTPLUS, PT_ACT_TANH = 0, 1
 PT_CELL_INT, PT_CELL_HGRU = 0, 1
@@ -68,6 +74,15 @@ class PtCellError(RuntimeError):
 
 _lock = threading.Lock()
 _lib = None
+
+
+def use_diag():
+    """Load the diagnostic library instead of the release one (tools only)."""
+    global LIB_PATH
+    with _lock:
+        if _lib is not None and LIB_PATH != DIAG_PATH:
+            raise PtCellError("the release library is already loaded in this process")
+        LIB_PATH = DIAG_PATH
 
 
 def load():

@@ -5,7 +5,10 @@ kernels — ``libptcell.so`` (InT / hGRU cell, include/pt_cell.h) and
 ``libptlstm.so`` (ConvLSTM cell, include/pt_lstm.h) — and ``g++`` for the host
 TFRecord reader ``libpttfr.so`` (include/pt_tfrecord.h, zlib).  They sit next
 to the ctypes bindings so they travel with the repository snapshot to the GPU
-box.
+box.  ``libptcell_diag.so`` is the same cell library built with -DPT_DIAG=1
+(the PT_CELL_ABLATE / PT_CELL_DEBUG_STOP switches and pt_cell_trace, for
+tools/ only: ``ptamd._lib.use_diag()``); the release ``libptcell.so`` ignores
+those switches.
 """
 from __future__ import annotations
 
@@ -20,11 +23,13 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INC = os.path.join(REPO, "include")
 
-# library -> (sources, extra dependencies)
+# library -> (sources, extra dependencies[, extra compiler flags])
+_CELL = ([os.path.join(CSRC, "pt_cell.hip"), os.path.join(CSRC, "pt_readout.hip")],
+         [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
+          os.path.join(INC, "pt_cell.h"), os.path.join(INC, "pt_readout.h")])
 LIBS = {
-    "libptcell.so": ([os.path.join(CSRC, "pt_cell.hip"), os.path.join(CSRC, "pt_readout.hip")],
-                     [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
-                      os.path.join(INC, "pt_cell.h"), os.path.join(INC, "pt_readout.h")]),
+    "libptcell.so": _CELL,
+    "libptcell_diag.so": _CELL + (["-DPT_DIAG=1"],),
     "libpttfr.so": ([os.path.join(CSRC, "pt_tfrecord.cpp")], [os.path.join(INC, "pt_tfrecord.h")]),
     "libptlstm.so": ([os.path.join(CSRC, "pt_lstm.hip")],
                      [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
@@ -44,7 +49,7 @@ def up_to_date(lib: str = "libptcell.so") -> bool:
     if not os.path.exists(out):
         return False
     t = os.path.getmtime(out)
-    srcs, deps = LIBS[lib]
+    srcs, deps = LIBS[lib][:2]
     return all(os.path.getmtime(d) <= t for d in srcs + deps)
 
 
@@ -53,7 +58,9 @@ def src_hash(lib: str) -> str:
     into its version string, so measurements (profiles/*_pmc_traffic.json) can
     be matched to the exact kernels that produced them."""
     h = hashlib.sha256(HIP_FLAGS.encode())
-    srcs, deps = LIBS[lib]
+    srcs, deps = LIBS[lib][:2]
+    for flag in (LIBS[lib][2] if len(LIBS[lib]) > 2 else []):
+        h.update(flag.encode())
     for f in srcs + deps:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
@@ -64,7 +71,8 @@ def src_hash(lib: str) -> str:
 def build(force: bool = False, verbose: bool = True) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     procs = []
-    for lib, (srcs, _) in LIBS.items():
+    for lib, spec in LIBS.items():
+        srcs, extra = spec[0], (spec[2] if len(spec) > 2 else [])
         if not force and up_to_date(lib):
             continue
         out = _out(lib)
@@ -72,7 +80,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
             cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared",
                    "-pthread", "-Wall", "-I", INC, "-o", out + ".tmp", *srcs, "-lz", "-ldl"]
         else:
-            cmd = [hipcc, *HIP_FLAGS.split(), "-fPIC", "-shared",
+            cmd = [hipcc, *HIP_FLAGS.split(), *extra, "-fPIC", "-shared",
                    f'-DPT_SRC_HASH="{src_hash(lib)}"', "-I", INC, "-o", out + ".tmp", *srcs]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -5,7 +5,12 @@ ptamd.dist.CellDist, against the single-process HIP cell.
 * SyncBN: 2 ranks x 2 clips with BatchNorm statistics all-reduced between
   the cell's launches reproduce the single process on all 4 clips (logits per
   clip, rank-averaged gradients) -- the library's per-reduction callback, the
-  SyncBN totals kernel and the global clip count in every consumer.
+  SyncBN totals kernel and the global clip count in every consumer; for the
+  f32 cell (split forward kernels) and the bf16 cell (the fused forward
+  segments, which read the all-rank totals through bnf_src; the banded
+  backward convs).  bf16 tolerance: the two-rank totals are the same fp64
+  sums in another association, so a bf16-stored value may round the other
+  way.
 * early-gradient overlap: with per-replica BatchNorm (the default) the
   gradients averaged in two parts -- the cell's early gradients on a side
   stream behind the event the backward records before its k x k
@@ -52,7 +57,7 @@ def _batch():
     return x, torch.tensor([ord(v) for v in labels], dtype=torch.float32)
 
 
-def _worker(rank, world, port, sync_bn, out_q):
+def _worker(rank, world, port, sync_bn, out_q, dtype="f32"):
     import sys
     sys.path[:0] = [os.path.join(REPO, "tests"), REPO, os.path.join(REPO, "pathtracker-models_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -62,6 +67,7 @@ def _worker(rank, world, port, sync_bn, out_q):
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = _model().to(dev)
+    m.cell_dtype = dtype
     x, y = _batch()
     sh = slice(2 * rank, 2 * rank + 2)
     bucket = GradBucket(m.parameters(), dev)
@@ -78,12 +84,12 @@ def _worker(rank, world, port, sync_bn, out_q):
     dist.destroy_process_group()
 
 
-def _run_ranks(sync_bn):
+def _run_ranks(sync_bn, dtype="f32"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, sync_bn, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sync_bn, q, dtype)) for r in range(2)]
     for p in procs:
         p.start()
     res = {r: rest for r, *rest in (q.get(timeout=200) for _ in range(2))}
@@ -93,9 +99,10 @@ def _run_ranks(sync_bn):
     return res
 
 
-def _single(x, y):
+def _single(x, y, dtype="f32"):
     dev = torch.device("cuda:0")
     m = _model().to(dev)
+    m.cell_dtype = dtype
     out, _ = m(x.to(dev))
     F.binary_cross_entropy_with_logits(out, y.to(dev).reshape(-1, 1)).backward()
     return out.detach().cpu(), {k: p.grad.detach().cpu() for k, p in m.named_parameters()
@@ -110,17 +117,18 @@ def _close_grads(got, ref, rel):
 
 
 @pytest.mark.timeout(300)
-def test_syncbn_two_ranks_equal_single_process():
+@pytest.mark.parametrize("dtype,atol,rel", [("f32", 1e-5, 1e-5), ("bf16", 2e-3, 2e-2)])
+def test_syncbn_two_ranks_equal_single_process(dtype, atol, rel):
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
-    res = _run_ranks(sync_bn=True)
+    res = _run_ranks(sync_bn=True, dtype=dtype)
     x, y = _batch()
-    lo, g = _single(x, y)
+    lo, g = _single(x, y, dtype)
     for r in (0, 1):
         logits, early, grads = res[r]
-        torch.testing.assert_close(torch.from_numpy(logits), lo[2 * r:2 * r + 2], rtol=0, atol=1e-5)
+        torch.testing.assert_close(torch.from_numpy(logits), lo[2 * r:2 * r + 2], rtol=0, atol=atol)
         assert early > 0                                 # the side-stream part ran
-        _close_grads(grads, g, 1e-5)
+        _close_grads(grads, g, rel)
 
 
 @pytest.mark.timeout(300)

@@ -1,23 +1,34 @@
-"""pt_cell_trace (diagnostics C-ABI, include/pt_cell.h): with a buffer set,
-one frame's point-wise and fused-forward launches stamp their phases with the
-100 MHz real-time counter, per sampled workgroup, in order; with the buffer
-cleared nothing is written and the results are unchanged (tools/trace.py
-reads the same records)."""
+"""Diagnostic switches (include/pt_cell.h).
+
+* The release library (libptcell.so) ignores them: with PT_CELL_ABLATE
+  (phase-skipping bits whose results are garbage) and PT_CELL_DEBUG_STOP set
+  in the environment, forward and backward are bit-identical to a run without
+  them, and pt_cell_trace is refused.
+* The diagnostic build (libptcell_diag.so, -DPT_DIAG=1, loaded by tools/ with
+  ptamd._lib.use_diag()): with a trace buffer set, one frame's point-wise and
+  fused-forward launches stamp their phases with the 100 MHz real-time
+  counter, per sampled workgroup, in order; with the buffer cleared nothing is
+  written and the results are unchanged (tools/trace.py reads the same
+  records).  Run in a child process, which loads the diagnostic library.
+"""
 import ctypes
+import os
+import subprocess
+import sys
 
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-def test_phase_stamps_are_written_in_order_and_change_nothing():
+
+def _setup():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     from models import InT
-    from ptamd import _lib
     dev = torch.device("cuda:0")
-    lib = _lib.load()
     torch.manual_seed(5)
     m = InT.InT(dimensions=32, timesteps=4, kernel_size=7).to(dev)
     m.cell_dtype = "bf16"
@@ -28,25 +39,71 @@ def test_phase_stamps_are_written_in_order_and_change_nothing():
         out, _ = m(x)
         out.sum().backward()
         torch.cuda.synchronize()
-        return out.detach().clone(), m.unit1.w_exc.grad.detach().clone()
+        return out.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()
+                                      if p.grad is not None}
+    return run
 
+
+def test_release_library_ignores_the_diagnostic_switches():
+    from ptamd import _lib
+    run = _setup()
+    lib = _lib.load()
+    assert "diag" not in lib.pt_version().decode()
     o0, g0 = run()
-    buf = torch.zeros(_lib.NKINDS * 256 * 16, dtype=torch.int64, device=dev)
-    lib.pt_cell_trace(ctypes.c_void_p(buf.data_ptr()), 1)
+    os.environ.update(PT_CELL_ABLATE=str(1 | 4 | 8 | 32 | 512), PT_CELL_DEBUG_STOP="2")
     try:
         o1, g1 = run()
     finally:
-        lib.pt_cell_trace(None, -1)
-    assert torch.equal(o0, o1) and torch.equal(g0, g1)
-    tr = buf.view(_lib.NKINDS, 256, 16).cpu()
-    for kind, slots in (("k_pw_bb", [0, 1, 2, 3, 4, 5, 6]), ("k_pw_ba", [0, 2, 3, 4, 5, 6]),
-                        ("k_fused_fa", [0, 2, 3, 4, 5, 6]), ("k_fused_fb", [0, 2, 3, 4, 5, 6])):
-        r = tr[_lib.KIND_NAMES.index(kind)]
-        live = r[:, 0] > 0
-        assert live.any(), kind
-        r = r[live][:, slots]
-        assert (r > 0).all(), kind
-        assert (r[:, 1:] >= r[:, :-1]).all(), kind            # phases in order per workgroup
-    buf.zero_()
-    run()                                                     # cleared: no stamps
-    assert int(buf.abs().sum()) == 0
+        os.environ.pop("PT_CELL_ABLATE")
+        os.environ.pop("PT_CELL_DEBUG_STOP")
+    assert torch.equal(o0, o1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+    assert lib.pt_cell_trace(None, -1) == 2                  # PT_ERR_UNSUPPORTED
+    assert b"diagnostic build" in lib.pt_last_error()
+
+
+_CHILD = r"""
+import ctypes, os, sys
+sys.path[:0] = [{repo!r}, os.path.join({repo!r}, "pathtracker-models_amd"), os.path.join({repo!r}, "tests")]
+import torch
+from ptamd import _lib
+_lib.use_diag()
+from test_gpu_trace import _setup
+run = _setup()
+lib = _lib.load()
+assert "diag" in lib.pt_version().decode()
+o0, g0 = run()
+dev = torch.device("cuda:0")
+buf = torch.zeros(_lib.NKINDS * 256 * 16, dtype=torch.int64, device=dev)
+assert lib.pt_cell_trace(ctypes.c_void_p(buf.data_ptr()), 1) == 0
+try:
+    o1, g1 = run()
+finally:
+    lib.pt_cell_trace(None, -1)
+assert torch.equal(o0, o1) and all(torch.equal(g0[k], g1[k]) for k in g0)
+tr = buf.view(_lib.NKINDS, 256, 16).cpu()
+for kind, slots in (("k_pw_bb", [0, 1, 2, 3, 4, 5, 6]), ("k_pw_ba", [0, 2, 3, 4, 5, 6]),
+                    ("k_fused_fa", [0, 2, 3, 4, 5, 6]), ("k_fused_fb", [0, 2, 3, 4, 5, 6])):
+    r = tr[_lib.KIND_NAMES.index(kind)]
+    live = r[:, 0] > 0
+    assert live.any(), kind
+    r = r[live][:, slots]
+    assert (r > 0).all(), kind
+    assert (r[:, 1:] >= r[:, :-1]).all(), kind            # phases in order per workgroup
+buf.zero_()
+run()                                                     # cleared: no stamps
+assert int(buf.abs().sum()) == 0
+print("trace ok")
+"""
+
+
+@pytest.mark.timeout(240)
+def test_diag_build_phase_stamps_are_written_in_order_and_change_nothing():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    env = dict(os.environ)
+    env.pop("PT_CELL_ABLATE", None)
+    r = subprocess.run([sys.executable, "-c", _CHILD.format(repo=REPO)], env=env, cwd=REPO,
+                       capture_output=True, text=True, timeout=220)
+    assert r.returncode == 0 and "trace ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

@@ -234,3 +234,25 @@ def test_param_staging_cache_reuses_its_buffer(dtype):
         p.add_(1)
     c = _as_f32(p)
     assert c is a and torch.equal(c, p.detach().float())
+
+
+def test_release_library_has_no_diagnostic_switches():
+    """The release libptcell.so never reads PT_CELL_ABLATE / PT_CELL_DEBUG_STOP
+    (compiled only into libptcell_diag.so, -DPT_DIAG=1) and refuses
+    pt_cell_trace, so a stray environment variable cannot alter training;
+    the diagnostic build keeps them for tools/ (host calls only, no GPU)."""
+    from ptamd import _lib
+    rel = open(_lib.LIB_PATH, "rb").read()
+    diag = open(_lib.DIAG_PATH, "rb").read()
+    for name in (b"PT_CELL_ABLATE", b"PT_CELL_DEBUG_STOP"):
+        assert name not in rel, name
+        assert name in diag, name
+    lib = _lib.load()
+    assert "diag" not in lib.pt_version().decode()
+    assert lib.pt_cell_trace(None, -1) == 2          # PT_ERR_UNSUPPORTED
+    assert b"diagnostic build" in lib.pt_last_error()
+    dl = ctypes.CDLL(_lib.DIAG_PATH)
+    dl.pt_version.restype = ctypes.c_char_p
+    assert "diag" in dl.pt_version().decode()
+    dl.pt_cell_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert dl.pt_cell_trace(None, -1) == 0

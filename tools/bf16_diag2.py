@@ -9,6 +9,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "pathtracker-models_amd"), os.path.join(REPO, "tests")]
 
+os.environ["PT_CELL_DIAG"] = "1"     # the PT_DIAG build honours PT_CELL_ABLATE
 import torch  # noqa: E402
 
 import bench  # noqa: E402

@@ -16,6 +16,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "pathtracker-models_amd")]
 import torch  # noqa: E402
 
 from ptamd import _lib  # noqa: E402
+_lib.use_diag()         # the PT_DIAG build (libptcell_diag.so) honours the switches
 from ptamd.cell import _desc, _pack, _ptr, _stream  # noqa: E402
 from models import InT  # noqa: E402
 
@@ -29,6 +30,8 @@ def al(x):
 def layout(B, T, es):
     o, r = 0, {}
     r["bnf_cnt"] = o; o += al(T * 2 * NGRP * 4)
+    r["bnf_done"] = o; o += al(T * 2 * 4)          # persistent forward counters (pt_cell.hip plan())
+    r["err"] = o; o += al(4)
     r["bnf_grp"] = o; o += al(T * 2 * NGRP * 96 * 8)
     r["bnf_part"] = o; o += al(T * 2 * B * 64 * 4)
     r["bnb_cnt"] = o; o += al(T * 2 * NGRP * 4)

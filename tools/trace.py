@@ -12,6 +12,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "pathtracker-models_amd")]
 import torch  # noqa: E402
 
 from ptamd import _lib  # noqa: E402
+_lib.use_diag()         # the PT_DIAG build (libptcell_diag.so) honours the switches
 from models import InT  # noqa: E402
 
 SLOTS = {"k_pw_bb": ["entry", "issued", "prologue", "rows", "bn_partial", "flush", "publish"],
