@@ -193,7 +193,7 @@ def adam_step(params: Params, grads: Params, lr: float = 3e-4, betas=(0.9, 0.999
 # ----------------------------------------------------------------------------- ConvLSTM
 
 def convlstm_forward(sd: Params, img: Tensor, timesteps: int, eps: float = 1e-3,
-                     with_jv: bool = False, mu: float = 0.9):
+                     with_jv: bool = False, mu: float = 0.9, create_graph: bool = False):
     """ConvLSTM on a static single-channel image (models/convlstm.py:116-147, bptt).
 
     conv0 (Gabor 7x7, 1->25, bias) then ``pow 2`` (:118-119); ``timesteps``
@@ -201,7 +201,8 @@ def convlstm_forward(sd: Params, img: Tensor, timesteps: int, eps: float = 1e-3,
     with bias, h-convs without); ``BN(h)`` (batch stats, :111,146) -> 1x1
     ``conv6`` 25->2 (:112,147).  Returns ``(output [B,2,H,W], h_T, c_T)``, or
     ``(output, h_T, c_T, jv_penalty)`` with ``with_jv`` (see
-    :func:`convlstm_jv_penalty`).
+    :func:`convlstm_jv_penalty`; ``create_graph``: the penalty keeps its graph,
+    as the reference's ``jacobian_penalty=True`` builds it, :158-162).
     """
     x = F.conv2d(img, sd["conv0.weight"], sd["conv0.bias"], padding=3).pow(2)
     k = sd["unit1.Wxi.weight"].shape[-1]
@@ -228,10 +229,10 @@ def convlstm_forward(sd: Params, img: Tensor, timesteps: int, eps: float = 1e-3,
     out = F.conv2d(out, sd["conv6.weight"], sd["conv6.bias"])
     if not with_jv:
         return out, h, c
-    return out, h, c, convlstm_jv_penalty(hs, cs, mu)
+    return out, h, c, convlstm_jv_penalty(hs, cs, mu, create_graph)
 
 
-def convlstm_jv_penalty(hs, cs, mu: float = 0.9) -> Tensor:
+def convlstm_jv_penalty(hs, cs, mu: float = 0.9, create_graph: bool = False) -> Tensor:
     """Training-mode Jacobian penalty of ConvLSTM (models/convlstm.py:150-161, l1):
 
         jv = clamp(J_h^T 1 - mu, 0)^2 + clamp(J_c^T 1 - mu, 0)^2
@@ -241,12 +242,16 @@ def convlstm_jv_penalty(hs, cs, mu: float = 0.9) -> Tensor:
     direct forget-gate term f_{T-1} and the path through h_{T-2} = o tanh(c_{T-2})
     into the next step's gates.  ``hs`` / ``cs`` are the per-step states of a
     graph that requires grad; needs ``timesteps >= 2`` (the reference's
-    ``state_2nd_last`` is unbound otherwise).
+    ``state_2nd_last`` is unbound otherwise).  ``create_graph`` (the reference's
+    ``jacobian_penalty=True``, :158-162): the penalty is returned with its graph,
+    so its parameter gradients (through the last step's Jacobian and, via
+    h_{T-2} / c_{T-2}, the earlier steps) reach a loss that adds it.
     """
     ones = torch.ones_like(hs[-1])
-    jh = torch.autograd.grad(hs[-1], hs[-2], ones, retain_graph=True)[0]
-    jc = torch.autograd.grad(cs[-1], cs[-2], ones, retain_graph=True)[0]
-    return ((jh - mu).clamp(0) ** 2 + (jc - mu).clamp(0) ** 2).detach()
+    jh = torch.autograd.grad(hs[-1], hs[-2], ones, retain_graph=True, create_graph=create_graph)[0]
+    jc = torch.autograd.grad(cs[-1], cs[-2], ones, retain_graph=True, create_graph=create_graph)[0]
+    jv = (jh - mu).clamp(0) ** 2 + (jc - mu).clamp(0) ** 2
+    return jv if create_graph else jv.detach()
 
 
 def flops_per_clip_frame(c: int = 32, h: int = 32, w: int = 32, k: int = 7) -> int:

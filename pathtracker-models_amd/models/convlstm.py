@@ -16,10 +16,17 @@ BN (:146), conv6 (:147) and the criterion stay in PyTorch.  The cell-level
 ``grad_method='rbp'`` (:124-135, Neumann-series backward in ``dummyhgru``)
 works unchanged on top of it.
 
-Differences from the reference, by design: ``jv_penalty`` is returned without
-a graph even when ``jacobian_penalty=True`` (the reference never adds it to the
-returned loss; differentiating it would need a double backward through the
-fused cell, which raises); the image must be 32x32 and ``filt_size`` odd <= 15.
+``jacobian_penalty=True`` (training, bptt): the reference builds the penalty
+with ``create_graph`` (:158-162), so a loss that adds it (mainclean.py:195)
+differentiates through the Jacobian of the last step.  The library runs the
+first T-2 steps; the last two run as PyTorch ops (``ConvLSTMCell.torch_step``,
+the reference's own cell arithmetic, :84-90) so that autograd holds the graph
+the penalty needs: J_h = d h_T / d h_{T-1} and J_c = d c_T / d c_{T-1}, the
+latter along every path (through h_{T-1} = o tanh c_{T-1} too), and their
+parameter gradients reach the earlier steps through h_{T-2}, c_{T-2} (the
+library's BPTT).  With the flag off ``jv_penalty`` is the library's detached
+value, as the reference's (create_graph=False).  The image must be 32x32 and
+``filt_size`` odd <= 15.
 """
 import os
 
@@ -119,6 +126,17 @@ class ConvLSTMCell(nn.Module):
         h_t, c_t, _ = self.steps(x, 1, h, c)
         return h_t, c_t
 
+    def torch_step(self, x, h, c):
+        """One step as PyTorch ops (reference convlstm.py:84-90): the graph the
+        ``jacobian_penalty=True`` penalty differentiates (double backward)."""
+        def gate(g, f):
+            return f(getattr(self, f"Wx{g}")(x) + getattr(self, f"Wh{g}")(h))
+        i_t = gate("i", torch.sigmoid)
+        f_t = gate("f", torch.sigmoid)
+        c_t = f_t * c + i_t * gate("c", torch.tanh)
+        o_t = gate("o", torch.sigmoid)
+        return o_t * torch.tanh(c_t), c_t
+
 
 class ConvLSTM(nn.Module):
     """Reference models/convlstm.py:93-166 (static-image ConvLSTM, 25 channels)."""
@@ -183,9 +201,12 @@ class ConvLSTM(nn.Module):
             if self.training and self.timesteps < 2:
                 raise RuntimeError("ConvLSTM training needs timesteps >= 2 (the reference's "
                                    "state_2nd_last is unbound otherwise, convlstm.py:140-161)")
-            internal_h, _, jv = self.unit1.steps(x, self.timesteps, want_jv=self.training)
-            if self.training:
-                jv_penalty = jv
+            if self.training and self.jacobian_penalty:
+                jv_penalty, internal_h = self._penalty_with_graph(x)
+            else:
+                internal_h, _, jv = self.unit1.steps(x, self.timesteps, want_jv=self.training)
+                if self.training:
+                    jv_penalty = jv
         else:
             raise ValueError(f"unknown grad_method {self.grad_method!r}")
 
@@ -197,6 +218,25 @@ class ConvLSTM(nn.Module):
         if testmode:
             return output, states, loss
         return output, jv_penalty, loss
+
+    def _penalty_with_graph(self, x):
+        """(jv_penalty with its graph, h_T): steps 1..T-2 in the library, the
+        last two in PyTorch ops (module docstring; reference :137-162)."""
+        lstm._require_device(x)              # the HIP path's rule: no CPU run of the model
+        t = self.timesteps
+        if t > 2:
+            h, c, _ = self.unit1.steps(x, t - 2)
+        else:
+            h = c = torch.zeros_like(x)
+        state_2nd_last, state_2nd_last_c = self.unit1.torch_step(x, h, c)
+        last_state, internal_c = self.unit1.torch_step(x, state_2nd_last, state_2nd_last_c)
+        ones = torch.ones_like(last_state)
+        jv = torch.autograd.grad(last_state, state_2nd_last, grad_outputs=[ones],
+                                 retain_graph=True, create_graph=True)[0]
+        jv_penalty = (jv - 0.90).clamp(0) ** 2
+        jv = torch.autograd.grad(internal_c, state_2nd_last_c, grad_outputs=[ones],
+                                 retain_graph=True, create_graph=True)[0]
+        return jv_penalty + (jv - 0.90).clamp(0) ** 2, last_state
 
 
 class ConvLSTMVideo(nn.Module):

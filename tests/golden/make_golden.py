@@ -200,12 +200,16 @@ def make_r3d(ref_r3d, tag, *, batch, t_len, seed=0):
     print(tag, "loss", float(out["loss"]))
 
 
-def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0):
+def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0, jacobian_penalty=False):
+    """jacobian_penalty=True: the penalty is built with create_graph
+    (convlstm.py:158-162) and the training loss is loss + 10 mean(jv_penalty),
+    as mainclean.py:191-195 forms it; the grads are those of that sum."""
     torch.manual_seed(3000 + seed)
     cwd = os.getcwd()
     os.chdir(REF)                     # gabor_serre.npy is opened relative to CWD (convlstm.py:105)
     try:
-        model = ref_clstm.ConvLSTM(timesteps=timesteps, filt_size=filt)
+        model = ref_clstm.ConvLSTM(timesteps=timesteps, filt_size=filt,
+                                   jacobian_penalty=jacobian_penalty)
     finally:
         os.chdir(cwd)
     g = torch.Generator().manual_seed(seed)
@@ -222,7 +226,10 @@ def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0):
     for k, v in model.state_dict().items():
         out["param." + k] = v.numpy().copy()
     o, jv, loss = model(img, 0, 0, target, crit)
-    loss.backward()
+    if jacobian_penalty:
+        (loss + jv.mean() * 1e1).backward()
+    else:
+        loss.backward()
     out["output"] = o.detach().numpy()
     out["loss"] = np.array(loss.item(), dtype=np.float32)
     out["jv_penalty"] = jv.detach().numpy()
@@ -230,7 +237,7 @@ def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0):
         if p.grad is not None:
             out["grad." + name] = p.grad.numpy().copy()
     out.update(img=img.numpy(), target=target.numpy(), cfg_timesteps=np.array(timesteps),
-               cfg_filt=np.array(filt))
+               cfg_filt=np.array(filt), cfg_jacobian_penalty=np.array(int(jacobian_penalty)))
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
     print(tag, "loss", float(out["loss"]))
 
@@ -329,6 +336,13 @@ def main():
                                                   timesteps=3, filt=15, seed=9),
             "convlstm_t2": lambda: make_convlstm(ref_clstm, "convlstm_t2", batch=3, timesteps=2,
                                                  filt=7, seed=10),
+            # jacobian_penalty=True: the penalty carries parameter gradients
+            # (create_graph, convlstm.py:158-162); at T=4 and at the shortest T=2
+            "convlstm_jvp": lambda: make_convlstm(ref_clstm, "convlstm_jvp", batch=2, timesteps=4,
+                                                  filt=7, seed=17, jacobian_penalty=True),
+            "convlstm_jvp_t2": lambda: make_convlstm(ref_clstm, "convlstm_jvp_t2", batch=2,
+                                                     timesteps=2, filt=5, seed=18,
+                                                     jacobian_penalty=True),
         }
         only = os.environ.get("GOLDEN_ONLY")          # comma-separated tags to (re)generate
         for tag, job in jobs.items():

@@ -75,6 +75,34 @@ def test_convlstm_bptt_grads_and_jv_f32(tag):
         _assert_close(f"grad {k}", got[k].cpu(), v, 1e-6, 1e-3)
 
 
+@pytest.mark.parametrize("tag", ["convlstm_jvp", "convlstm_jvp_t2"])
+def test_convlstm_jacobian_penalty_with_graph_f32(tag):
+    """jacobian_penalty=True: the penalty carries its graph (convlstm.py:158-162)
+    and the loss is loss + 10 mean(jv_penalty) (mainclean.py:191-195); the
+    reference's gradients of that sum within 1e-3 (golden from the reference
+    with the flag set)."""
+    from models import convlstm as cl
+    dev = _dev()
+    g = load(tag)
+    m = cl.ConvLSTM(timesteps=int(g["cfg_timesteps"]), filt_size=int(g["cfg_filt"]),
+                    jacobian_penalty=True)
+    m.load_state_dict(params(g), strict=True)
+    m = m.to(dev).train()
+    img = torch.from_numpy(g["img"]).to(dev)
+    tgt = torch.from_numpy(g["target"]).to(dev)
+    out, jv, loss = m(img, 0, 0, tgt, torch.nn.CrossEntropyLoss())
+    assert jv.requires_grad
+    (loss + jv.mean() * 1e1).backward()
+    _assert_close("train output", out.detach().cpu(), g["output"], 1e-3)
+    assert abs(loss.item() - float(g["loss"])) < 1e-4
+    _assert_close("jv_penalty", jv.detach().cpu(), g["jv_penalty"], 1e-4, 1e-3)
+    ref = {k[len("grad."):]: v for k, v in g.items() if k.startswith("grad.")}
+    got = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
+    assert set(got) == set(ref), set(got) ^ set(ref)
+    for k, v in ref.items():
+        _assert_close(f"grad {k}", got[k].cpu(), v, 1e-6, 1e-3)
+
+
 def test_convlstm_bf16_tolerance():
     """bf16 operands / saved h, f32 gate math and accumulation, k=15: outputs
     (after the batch-statistics BN, which amplifies h's rounding) within 3 %

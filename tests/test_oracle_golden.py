@@ -92,6 +92,26 @@ def test_convlstm_static(tag):
         _close(leaf[k[len("grad."):]].grad, g[k], rtol=1e-4, atol=1e-7)
 
 
+@pytest.mark.parametrize("tag", ["convlstm_jvp", "convlstm_jvp_t2"])
+def test_convlstm_jacobian_penalty_with_graph(tag):
+    """jacobian_penalty=True (models/convlstm.py:158-162, create_graph): the
+    gradients of loss + 10 mean(jv_penalty) (mainclean.py:191-195)."""
+    g = load(tag)
+    assert int(g["cfg_jacobian_penalty"]) == 1
+    sd = params(g)
+    img = torch.from_numpy(g["img"])
+    target = torch.from_numpy(g["target"])
+    steps = int(g["cfg_timesteps"])
+    leaf = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    out, _, _, jv = cells.convlstm_forward(leaf, img, steps, with_jv=True, create_graph=True)
+    _close(jv.detach(), g["jv_penalty"], rtol=1e-4, atol=1e-6)
+    loss = torch.nn.functional.cross_entropy(out, target)
+    (loss + jv.mean() * 1e1).backward()
+    _close(loss.item(), float(g["loss"]))
+    for k in (k for k in g if k.startswith("grad.")):
+        _close(leaf[k[len("grad."):]].grad, g[k], rtol=1e-4, atol=1e-7)
+
+
 def test_flop_model():
     # SURVEY.md §8(d): 218,103,808 FLOP per clip-frame forward at C=32, 32x32, k=7
     assert cells.flops_per_clip_frame() == 218_103_808
