@@ -437,7 +437,15 @@ struct CellArgs {
   // 0.97 vs the f32 cell; rounding I, gE, eg, c_i or c_e instead moved none of
   // them below 0.998: tools/bf16_diag2.py).
   float* E;
-  S *I, *gE, *ci, *ce, *eg;
+  // I is f32 in both modes too (r04): stored in bf16 it carried most of the bf16
+  // cell's deviation from the f32 cell at the headline size with trained
+  // parameters (logits 2.1e-3 of 2.2e-3, i-gate bias gradient cosine 0.990;
+  // profiles/r04_bf16_attrib_trained.json).  Ic is I_t in the storage type, the
+  // exc conv's input and k_wgrad's X operand (bf16: a copy written beside I;
+  // f32: I itself).
+  float* I;
+  S* Ic;
+  S *gE, *ci, *ce, *eg;
   S* at;                                // hGRU only: attention map per frame (the gated inhibition)
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
   // BatchNorm reductions (see BnSlot), slot (t, bn) = t * 2 + bn:
@@ -1362,14 +1370,14 @@ __device__ float bn_bwd_partial(float s0, float s1, float* red, const BnSlot& ou
 //           eg = sig(e_w I_{t-1} + e_u gE) (:171, uses the OLD inhibition;
 //           no_inh: e_w E_{t-1}, :168)
 // -------------------------------------------------------------------------
-template <class S> struct FaIn { Pk<S> Iv, egv, cev; f32x16 Eo; };
+template <class S> struct FaIn { Pk<S> egv, cev; f32x16 Iv, Eo; };
 template <class S>
 __device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
   const size_t fs = fr_off(1, a.B);
   FaIn<S> w;
-  w.Iv = zero_pk<S>(); w.Eo = zero16(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
+  w.Iv = zero16(); w.Eo = zero16(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
   if (t > 0) {
-    w.Iv = load_pk(a.I + (t - 1) * fs + ro, c, h);
+    w.Iv = load_cl(a.I + (t - 1) * fs + ro, c, h);
     if (t >= 2) w.Eo = load_cl(a.E + (t - 2) * fs + ro, c, h);
     w.egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
     w.cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
@@ -1495,15 +1503,15 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
 //   (:162), ig = sig(i_w x + i_u I) (:165), I_t = (1-ig) I + ig Ihat (:166)
 //   [no_inh: I_t = gE (:168)]
 // -------------------------------------------------------------------------
-template <class S> struct FbIn { Pk<S> civ, Iv, gi; };
+template <class S> struct FbIn { Pk<S> civ, gi; f32x16 Iv; };
 template <class S, int HG>
 __device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
   const size_t fs = fr_off(1, a.B);
   FbIn<S> w;
   w.civ = load_pk(a.ci + t * fs + ro, c, h);
-  w.Iv = t > 0 ? load_pk(a.I + (t - 1) * fs + ro, c, h) : zero_pk<S>();
+  w.Iv = t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16();
   if constexpr (HG) w.gi = load_pk(a.at + t * fs + ro, c, h);   // gated inhibition att_t
-  else w.gi = w.Iv;                                             // InT: I_{t-1}
+  else w.gi = zero_pk<S>();                                     // InT: I_{t-1} (Iv, f32)
   return w;
 }
 
@@ -1526,11 +1534,13 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float*
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const float cn = A0 * (float)in.civ[r] + B0;
-    ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * (float)in.gi[r] + mu)));
+    const float gv = HG ? (float)in.gi[r] : in.Iv[r];
+    ih[r] = Act<ACT>::f(xv[r] - Act<ACT>::f(cn * (al * gv + mu)));
   }
   F pax[Tr<S>::KS], pai[Tr<S>::KS];
   cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
-  cl_to_pa<S>(wscr, in.gi, lane, pai, RND_G(a));
+  if constexpr (HG) cl_to_pa<S>(wscr, in.gi, lane, pai, RND_G(a));
+  else cl_to_pa<S>(wscr, in.Iv, lane, pai, RND_G(a));
   f32x16 acc = zero16();
   acc = gemm_pa<S>(pax, a.gf[2], acc, lane);
   acc = gemm_pa<S>(pai, a.gf[3], acc, lane);
@@ -1538,12 +1548,13 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float*
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const float ig = sigm_b(acc[r], nbi);
-    In[r] = (1.f - ig) * (float)in.Iv[r] + ig * ih[r];
+    In[r] = (1.f - ig) * in.Iv[r] + ig * ih[r];
   }
   if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 4096))
 #pragma unroll
     for (int r = 0; r < 16; ++r) In[r] = (float)(bf16_t)In[r];
   store_cl(a.I + t * fs + ro, c, h, In);
+  if constexpr (sizeof(S) == 2) store_cl(a.Ic + t * fs + ro, c, h, In);
   if (tile) tile_put_cl(tile, y, c, h, In);
 }
 
@@ -1567,6 +1578,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = (float)g[r];
       store_cl(a.I + t * fs + ro, c, h, v);
+      if constexpr (sizeof(S) == 2) store_cl(a.Ic + t * fs + ro, c, h, v);
     }
     return;
   }
@@ -1914,7 +1926,7 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
 //   dI_{t-1}, dgE partial.
 // -------------------------------------------------------------------------
 template <class S>
-struct BbRow { Pk<S> ginh, Iprev, dep, gEv, dIt, civ; };
+struct BbRow { f32x16 ginh, Iprev; Pk<S> dep, gEv, dIt, civ; };
 
 // Body of k_pw_bb (RPP = 1 row per wave, PWB_WGPC workgroups per clip).
 template <class S, int ACT, int HG, int RPP>
@@ -1937,14 +1949,14 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
   // and I_{t-1} is a separate tile.
   auto load_row = [&](size_t ro, int c, int h) {
     BbRow<S> w;
-    w.Iprev = zero_pk<S>();
+    w.Iprev = zero16();
     if constexpr (HG) {
-      w.ginh = load_pk(a.at + t * fs + ro, c, h);
-      if (t > 0) w.Iprev = load_pk(a.I + (t - 1) * fs + ro, c, h);
+      w.ginh = load_cl(a.at + t * fs + ro, c, h);
+      if (t > 0) w.Iprev = load_cl(a.I + (t - 1) * fs + ro, c, h);
     } else {
-      if (t == 0) w.ginh = zero_pk<S>();
-      else if (a.no_inh) w.ginh = to_pk<S>(load_cl(a.E + (t - 1) * fs + ro, c, h));
-      else w.ginh = load_pk(a.I + (t - 1) * fs + ro, c, h);
+      if (t == 0) w.ginh = zero16();
+      else if (a.no_inh) w.ginh = load_cl(a.E + (t - 1) * fs + ro, c, h);
+      else w.ginh = load_cl(a.I + (t - 1) * fs + ro, c, h);
     }
     w.dep = load_pk(a.dEp + ro, c, h);
     w.gEv = load_pk(a.gE + t * fs + ro, c, h);
@@ -1990,10 +2002,10 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
     BbRow<S> w;
     if constexpr (RPP == 1) w = pre;
     else w = load_row(ro, c, h);
-    const Pk<S>& ginh = w.ginh;
+    const f32x16& ginh = w.ginh;
     const Pk<S>& dIt = w.dIt;
     const Pk<S>& civ = w.civ;
-    Pk<S>& Iprev = w.Iprev;
+    f32x16& Iprev = w.Iprev;
     F pe[Tr<S>::KS];
     {
       f32x16 depf;
@@ -2037,8 +2049,8 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
       f32x16 dIp, dip, dx;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float Ir = (float)ginh[r], dIr = (float)dIt[r];
-        const float Ip = HG ? (float)Iprev[r] : Ir;      // I_{t-1} of the update (:166)
+        const float Ir = ginh[r], dIr = (float)dIt[r];
+        const float Ip = HG ? Iprev[r] : Ir;             // I_{t-1} of the update (:166)
         const float xi = ((float)civ[r] - m0) * rs0;
         const float cn = A0 * (float)civ[r] + B0;
         const float u = al * Ir + mu;
@@ -2059,7 +2071,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         // InT: dI_{t-1} collects the update and the gated-inhibition terms;
         // hGRU: the gated-inhibition terms go to att (dA, kept in dIp's slot)
         dIp[r] = HG ? du * al : dIr * (1.f - ig) + du * al;
-        if constexpr (HG) Iprev[r] = (S)(dIr * (1.f - ig));
+        if constexpr (HG) Iprev[r] = dIr * (1.f - ig);
         sm[0] += du * Ir;
         sm[1] += du;
         sm[2] += dip[r];
@@ -2095,7 +2107,7 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
         store_cl(a.dAt + ro, c, h, dIp);
         f32x16 gi;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) gi[r] = (float)Iprev[r];
+        for (int r = 0; r < 16; ++r) gi[r] = Iprev[r];
         store_cl(a.GI + ro, c, h, gi);
       } else {
         store_cl(a.GI + ro, c, h, rb16(RND_T(a), dIp));
@@ -2410,7 +2422,7 @@ __global__ __launch_bounds__((wgrad_nt<S, PAD>()), 1) void k_wgrad(CellArgs<S> a
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = blockIdx.x, conv = blockIdx.y + conv0, grp = blockIdx.z;
   const int KK = a.K * a.K;
-  const S* Xs = conv == 0 ? a.gE : a.I;
+  const S* Xs = conv == 0 ? a.gE : a.Ic;
   const S* Ds = conv == 0 ? a.dci_s : a.dce_s;
 
   float* dst = wslab + ((size_t)conv * nwg + g) * KK * 1024;
@@ -2859,7 +2871,7 @@ struct Plan {
   size_t es;          // element size of S
   size_t frame;       // elements per frame tensor (B*NPIX*C)
   // saved offsets
-  size_t o_E, o_I, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], o_pad, saved;
+  size_t o_E, o_I, o_Ic, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], o_pad, saved;
   // workspace offsets
   size_t o_bnf_cnt, o_bnf_part, o_bnf_grp, o_bnb_cnt, o_bnb_part, o_bnb_grp;   // BnSlot storage
   size_t o_bnf_done, o_err;   // persistent forward: group-sum counters [T][2], give-up flag
@@ -2897,12 +2909,13 @@ Plan plan(const pt_cell_desc* d) {
   const size_t fbytes = al(p.frame * p.T * p.es);
   size_t o = 0;
   p.o_E = o; o += al(p.frame * p.T * 4);          // f32 in both modes (CellArgs::E)
-  p.o_I = o; o += fbytes;
+  p.o_I = o; o += al(p.frame * p.T * 4);          // f32 in both modes (CellArgs::I)
   p.o_gE = o; o += fbytes;
   p.o_ci = o; o += fbytes;
   p.o_ce = o; o += fbytes;
   p.o_eg = o; o += fbytes;
   p.o_at = o; o += d->cell == PT_CELL_HGRU ? fbytes : 0;
+  p.o_Ic = o; o += p.es == 2 ? fbytes : 0;         // bf16 copy of I (f32: I itself)
   p.o_bnstat = o; o += al((size_t)p.T * 128 * 4);
   for (int i = 0; i < 4; ++i) { p.o_wf[i] = o; o += al((size_t)C * C * p.K * p.K * p.es); }
   for (int i = 0; i < 12; ++i) { p.o_g[i] = o; o += al((size_t)C * C * p.es); }
@@ -2958,7 +2971,8 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
     a.gf[i] = (const F*)(saved + p.o_g[i]);
     a.gt[i] = (const F*)(saved + p.o_g[6 + i]);
   }
-  a.E = (float*)(saved + p.o_E); a.I = (S*)(saved + p.o_I); a.gE = (S*)(saved + p.o_gE);
+  a.E = (float*)(saved + p.o_E); a.I = (float*)(saved + p.o_I);
+  a.Ic = p.es == 2 ? (S*)(saved + p.o_Ic) : (S*)(saved + p.o_I); a.gE = (S*)(saved + p.o_gE);
   a.ci = (S*)(saved + p.o_ci); a.ce = (S*)(saved + p.o_ce); a.eg = (S*)(saved + p.o_eg);
   a.at = a.hgru ? (S*)(saved + p.o_at) : nullptr;
   a.bnstat = (float*)(saved + p.o_bnstat);
@@ -3236,7 +3250,7 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
         if (int rc = bn_sync(dist, ca.bnout.grp, bn_ngrp(p.B), 96, ((size_t)t * 2 + 0) * 96, st)) return rc;
     }
     timed(PT_K_PW_FB, st, [&] { PW_LAUNCH(k_pw_fb, gpf, lpf); });
-    cb.src = a.I + t * fs; cb.out_raw = a.ce + t * fs; cb.bnout = bnf_slot(a, t, 1);
+    cb.src = a.Ic + t * fs; cb.out_raw = a.ce + t * fs; cb.bnout = bnf_slot(a, t, 1);
     timed(PT_K_CONV_FB, st, [&] {
       launch_conv_fwd<S>(p, st, cb); });
     if (syncbn(dist))

@@ -303,16 +303,22 @@ __device__ __forceinline__ float hsum16(const f32x16& v) {
 // range fix-up (cmp + cndmask + ldexp) around every call; no argument here
 // needs it (results that would be denormal flush to 0, which is harmless for
 // 1 + e^x, sigmoid and tanh).
-__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
-__device__ __forceinline__ float flog(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
-__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// (r04: each transcendental as inline asm with a wait state on either side
+// was tried against the run-to-run divergence and did not remove it; the cause
+// was the packed-FP32 pair reads, DESIGN.md §4 / ptamd/build.py.)
+__device__ __forceinline__ float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float hw_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fexp(float x) { return hw_exp2(x * 1.4426950408889634f); }
+__device__ __forceinline__ float flog(float x) { return hw_log2(x) * 0.6931471805599453f; }
+__device__ __forceinline__ float frcp(float x) { return hw_rcp(x); }
 __device__ __forceinline__ float sigm(float x) { return frcp(1.f + fexp(-x)); }
 // sigmoid(x + b) with nb = sig_nb(b) precomputed: the bias add and the 2^x
 // scaling fold into one FMA
 constexpr float L2E = 1.4426950408889634f;
 __device__ __forceinline__ float sig_nb(float b) { return -b * L2E; }
 __device__ __forceinline__ float sigm_b(float x, float nb) {
-  return frcp(1.f + __builtin_amdgcn_exp2f(fmaf(x, -L2E, nb)));
+  return frcp(1.f + hw_exp2(fmaf(x, -L2E, nb)));
 }
 __device__ __forceinline__ float ftanh(float x) {
   const float t = 1.f - 2.f * frcp(fexp(2.f * fabsf(x)) + 1.f);

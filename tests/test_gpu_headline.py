@@ -4,23 +4,24 @@ T=64 frames, bf16 cell) and the 64-frame recurrence in exact arithmetic.
 * bf16 vs f32 at B=256, T=64: the f32 HIP path is pinned to the reference at
   1e-3 (test_gpu_parity.py goldens; the oracle below), so at sizes the
   CPU oracle cannot reach quickly it is the reference.  Asserted: logits within
-  BF16_LOGIT_TOL; train (> 0.5, misc_functions.py:41) and eval (> 0,
-  test_model.py:127) decisions identical for every clip whose f32 logit is
-  farther than BF16_LOGIT_TOL from the threshold; gradient cosine over all
+  BF16_LOGIT_TOL = 1e-3 (north_star's bound); train (> 0.5, misc_functions.py:41)
+  and eval (> 0, test_model.py:127) decisions identical for EVERY clip, the
+  ones within the tolerance of a threshold included; gradient cosine over all
   parameters (each tensor scaled by its f32 norm) >= 0.995 and per tensor >=
-  BF16_GRAD_COS.  Run on the bench's own init (seed 1234), on parameters moved
-  off init, and on parameters trained for 300 bf16 steps on the bench's clips
-  (tests/golden/int_trained_headline.npz, tools/probe_headline.py --steps 300
-  --lr 2e-3).  The per-tensor floor is set by the trained case: the i-gate
-  bias gradient there (a 32-vector summed over 16.7M cancelling terms, formed
-  in f32 from the bf16-stored recurrence) measured cosine 0.983 (init 0.9987,
-  perturbed 0.9993; profiles/r03_parity_records.json).
+  BF16_GRAD_COS = 0.99.  Run on the bench's own init (seed 1234), on parameters
+  moved off init, and on parameters trained for 300 bf16 steps on the bench's
+  clips (tests/golden/int_trained_headline.npz, tools/probe_headline.py --steps
+  300 --lr 2e-3).  The trained case set the r03 bounds (2.5e-3, 0.98): the
+  inhibition I stored in bf16 carried most of the deviation
+  (profiles/r04_bf16_attrib_trained.json); with I in f32 (r04) it measures
+  logits 1.6e-4 and an i-gate bias gradient cosine of 0.996.
 * final classification accuracy at the headline size in exact arithmetic: the
   trained parameters with the readout's Linear(1,1) rescaled so that the 256
   logits span 4 units around 0.25 (>= 25 % of the clips on each side of both
   thresholds): f32 HIP vs the CPU oracle on the same clips -- logits within
   1e-3 and every train / eval decision identical; bf16 vs f32 there: no flip
-  outside the rescaled bf16 band (the rescale multiplies the bf16 error).
+  at all, the clips inside the rescaled bf16 band included (the rescale
+  multiplies the bf16 error; the record keeps the closest f32 margin).
 * f32 HIP vs the CPU oracle at T=64, B=8: logits 1e-3, every gradient
   1e-6 + 1e-3 max|g|.
 * hipGraph replay with poisoned buffers at B=256, T=64, bf16 (the config of
@@ -47,10 +48,11 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 B, T = 256, 64
-# bf16 vs f32 logit bound at B=256, T=64: measured 6.8e-4 (perturbed init),
-# 2.2e-3 (trained 300 steps; profiles/r03_parity_records.json)
-BF16_LOGIT_TOL = 2.5e-3
-BF16_GRAD_COS = 0.98
+# bf16 vs f32 logit bound at B=256, T=64 (north_star: 1e-3): with I stored
+# in f32 (r04) measured 1.6e-4 on the trained parameters (r03, bf16 I: 2.2e-3;
+# profiles/r04_parity_records.json)
+BF16_LOGIT_TOL = 1e-3
+BF16_GRAD_COS = 0.99
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -117,8 +119,9 @@ def test_bf16_matches_f32_at_headline_config(perturb):
     flips = {}
     for name, thr in (("train_0.5", 0.5), ("eval_0", 0.0)):
         far = (lo32 - thr).abs() > BF16_LOGIT_TOL
-        flips[name] = int(((lo16 > thr) != (lo32 > thr))[far].sum())
+        flips[name] = int(((lo16 > thr) != (lo32 > thr)).sum())      # every clip, in-band too
         stats[f"decided_clips_{name}"] = int(far.sum())
+        stats[f"in_band_clips_{name}"] = int((~far).sum())
     cos, cat16, cat32 = {}, [], []
     for k in g32:
         a, b = g16[k], g32[k]
@@ -127,7 +130,7 @@ def test_bf16_matches_f32_at_headline_config(perturb):
             cat16.append(a / b.norm())
             cat32.append(b / b.norm())
     a, b = torch.cat(cat16), torch.cat(cat32)
-    stats["flips_away_from_threshold"] = flips
+    stats["flips_all_clips"] = flips
     stats["grad_cosine_all"] = float(a @ b / (a.norm() * b.norm()))
     stats["grad_cosine_min"] = min(cos.values())
     stats["grad_cosine_min_tensor"] = min(cos, key=cos.get)
@@ -176,10 +179,13 @@ def test_headline_accuracy_f32_bit_identical_to_oracle():
         far16 = (lo32 - thr).abs() > band16
         rec[f"bf16_flips_{name}"] = int(((lo16 > thr) != (lo32 > thr))[far16].sum())
         rec[f"bf16_in_band_{name}"] = int((~far16).sum())
+        # every clip, the in-band ones included
+        rec[f"bf16_flips_all_{name}"] = int(((lo16 > thr) != (lo32 > thr)).sum())
+        rec[f"bf16_closest_f32_margin_{name}"] = float((lo32 - thr).abs().min())
     _record("headline_accuracy_B256_T64_trained_rescaled", rec)
     assert err <= 1e-3, rec
     for thr in ("train_0.5", "eval_0"):
-        assert rec[f"f32_flips_{thr}"] == 0 and rec[f"bf16_flips_{thr}"] == 0, rec
+        assert rec[f"f32_flips_{thr}"] == 0 and rec[f"bf16_flips_all_{thr}"] == 0, rec
         assert 0.25 * B <= rec[f"above_{thr}"] <= 0.75 * B, rec     # straddles the threshold
 
 

@@ -141,8 +141,9 @@ def test_u8_clips_match_f32_input():
 def test_bf16_matches_f32_at_cfg3_size():
     """The clip ConvLSTM at its bench size (B=256, T=64, k=7): the bf16 cell
     against the f32 cell (itself pinned to the oracle above) on the bench's
-    clips — logits within 5e-2, identical 0.5 / 0 decisions for every clip
-    farther than that from the threshold, per-tensor gradient cosine >= 0.99."""
+    clips — logits within 1e-3 (north_star's bound; measured 3.4e-4), identical
+    0.5 / 0 decisions for every clip (in-band ones included), per-tensor
+    gradient cosine >= 0.99."""
     from models import convlstm
     dev = _dev()
     x, y = _clips(1000, 256, 64)
@@ -161,17 +162,16 @@ def test_bf16_matches_f32_at_cfg3_size():
         res[dt] = (out.detach().double().flatten().cpu(),
                    {n: p.grad.detach().double().flatten().cpu() for n, p in m.named_parameters()})
     (o32, g32), (o16, g16) = res["f32"], res["bf16"]
-    tol = 5e-2
+    tol = 1e-3
     err = float((o16 - o32).abs().max())
     cos = {n: float(g16[n] @ g32[n] / (g16[n].norm() * g32[n].norm()))
            for n in g32 if g32[n].norm() > 1e-12}
     flips = {}
     for name, thr in (("train_0.5", 0.5), ("eval_0", 0.0)):
-        far = (o32 - thr).abs() > tol
-        flips[name] = int(((o16 > thr) != (o32 > thr))[far].sum())
+        flips[name] = int(((o16 > thr) != (o32 > thr)).sum())
     rec = {"logit_max_abs_err": err, "logit_spread": float(o32.max() - o32.min()),
            "grad_cosine_min": min(cos.values()), "grad_cosine_min_tensor": min(cos, key=cos.get),
-           "flips_away_from_threshold": flips}
+           "flips_all_clips": flips}
     from goldens import record
     record("convlstm_video_bf16_vs_f32_B256_T64", rec)
     assert err <= tol, rec

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 mkdir -p exp
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DPT_SRC_HASH="\"exp-$name\"" $flags \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -fPIC -shared -DPT_SRC_HASH="\"exp-$name\"" $flags \
     -I include -o exp/libptcell_$name.so pathtracker-models_amd/csrc/pt_cell.hip pathtracker-models_amd/csrc/pt_readout.hip 2>/dev/null &
 done
 wait

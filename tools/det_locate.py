@@ -78,16 +78,16 @@ def explain(w0, w1, saved, L, B, T, m, t):
     frame = B * 1024 * 32
     fb = al(frame * T * es)
     o_E = 0
-    o_I = al(frame * T * 4)
-    o_ce = o_I + 3 * fb
+    o_I = al(frame * T * 4)                 # I f32 (r04), then gE, ci, ce, eg, [at], Ic (bf16)
+    o_ce = o_I + al(frame * T * 4) + 2 * fb
     o_eg = o_ce + fb
-    o_bn = o_eg + fb
+    o_bn = o_eg + fb + (fb if es == 2 else 0)
     bf = lambda buf, off, n: buf[off:off + n * 2].view(torch.bfloat16).float()
     nb = frame * es
     d0 = w0[L["dcE"]:L["dcE"] + nb].view(torch.bfloat16).float().view(B, 32, 32, 32)
     d1 = w1[L["dcE"]:L["dcE"] + nb].view(torch.bfloat16).float().view(B, 32, 32, 32)
     dEn = w1[L["dEn"]:L["dEn"] + nb].view(torch.bfloat16).float().view(B, 32, 32, 32)
-    I = bf(saved, o_I + t * nb, frame).view(B, 32, 32, 32)
+    I = saved[o_I + t * frame * 4:o_I + (t + 1) * frame * 4].view(torch.float32).view(B, 32, 32, 32)
     ce = bf(saved, o_ce + t * nb, frame).view(B, 32, 32, 32)
     eg = bf(saved, o_eg + t * nb, frame).view(B, 32, 32, 32)
     st = saved[o_bn:o_bn + T * 128 * 4].view(torch.float32).view(T, 128)[t]
@@ -109,8 +109,21 @@ def explain(w0, w1, saved, L, B, T, m, t):
         px = sorted({p for p, _ in diff})
         ch = sorted({c for _, c in diff})
         samp = [(p, c, float(d0[b, y, p, c]), float(d1[b, y, p, c]), float(exp_[p, c])) for p, c in diff[:6]]
+        # raw per-element record of every differing element (tools: which input
+        # of the head, if replaced, reproduces the deviating run's outputs)
+        E_prev = saved[o_E + (t - 1) * frame * 4:o_E + t * frame * 4].view(torch.float32).view(B, 32, 32, 32)
+        tr = {n: (w0[L[n]:L[n] + nb].view(torch.bfloat16).float().view(B, 32, 32, 32),
+                  w1[L[n]:L[n] + nb].view(torch.bfloat16).float().view(B, 32, 32, 32)) for n in ("dcE", "dIl", "dEp", "dEn")}
+        raw = []
+        for p, c in diff[:16]:
+            raw.append({"p": p, "c": c, "I": float(I[b, y, p, c]), "ce": float(ce[b, y, p, c]),
+                        "eg": float(eg[b, y, p, c]), "Eo": float(E_prev[b, y, p, c]),
+                        "kap": float(kap[c]), "gam": float(gam[c]), "bw1": float(bw1[c]), "bb1": float(bb1[c]),
+                        "m1": float(m1[c]), "rs1": float(rs1[c]),
+                        "I_row": I[b, y, :, c].tolist(), "ce_row": ce[b, y, :, c].tolist(),
+                        **{f"{n}_{k}": float(v[k][b, y, p, c]) for n, v in tr.items() for k in (0, 1)}})
         out.append({"clip": b, "row": y, "n_diff": len(diff), "px": px, "ch": ch,
-                    "maxerr_run0": e0, "maxerr_run1": e1, "samples": samp})
+                    "maxerr_run0": e0, "maxerr_run1": e1, "samples": samp, "raw": raw})
     return out
 
 
