@@ -17,6 +17,7 @@
 // partial sums (fp64 atomics), the next kernel finalises them (kernel boundary
 // = grid-wide sync).  See DESIGN.md §3.
 #include "pt_device.h"
+#include "pt_pr.h"
 #include "pt_graph.h"
 #include "../../include/pt_cell.h"
 
@@ -430,6 +431,9 @@ struct CellArgs {
   const F *wf_inh, *wf_exc, *wt_inh, *wt_exc;   // conv fragments (fwd, transposed)
   const F* gf[6];                       // 1x1 fragments, forward
   const F* gt[6];                       // 1x1 fragments, transposed (backward)
+  using F16 = typename T16<S>::frag;
+  const F16* g16f[6];                   // the same as 16x16 B operands (k_pw_bb2, pt_pr.h)
+  const F16* g16t[6];
   // Saved per frame [T][B][32][32][32].  E is f32 in both modes: stored in
   // bf16 it stagnates once the excitation settles (|eg (Ehat - E)| below half
   // a bf16 ulp of E), and the gate gradients, which measure that slow
@@ -2140,6 +2144,313 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   pw_bb_body<S, ACT, HG, PWB_RPP>(a, smem, blockIdx.x / PWB_WGPC, blockIdx.x % PWB_WGPC);
 }
 
+// =========================================================================
+// k_pw_bb2 (r04): backward point-wise B in the half-row PR layout (pt_pr.h).
+// Same arithmetic as k_pw_bb (models/InT.py:162-171 differentiated, the
+// reference's autograd of rCell.forward).  A workgroup = 8 waves owns 8 image
+// rows of one clip, in two sets of 4 rows; in each set wave w takes one half
+// row (row w >> 1 of the set, pixels 16 (w & 1) .. +15), 8 values per lane,
+// <= 128 VGPRs: 4 waves per SIMD (k_pw_bb: 2) and half the workgroups of
+// k_pw_bb, so a launch is two rounds of workgroups instead of four and each
+// workgroup's prologue and epilogue serve twice the rows.  Per half row: the
+// tiles loaded once, the 1x1 gates as 16x16x32 MFMAs (A operand
+// transposed through a per-wave LDS scratch), the 1x1 weight-gradient
+// operands staged channel-major; after each set wave w contracts output tile
+// row (w & 1) of gate w >> 1 (i_w, i_u, e_w, e_u) over the set's 128 pixels
+// into registers.  At the end the per-channel sums (lane-local, xor 16 / 32,
+// then the 8 waves in order) and the gate tiles go to the slab (old values
+// loaded at entry).  BatchNorm producers: PB2_WGPC workgroups per clip.
+// =========================================================================
+constexpr int PB2_NT = 512, PB2_NW = PB2_NT / 64;
+constexpr int PB2_SET = 4;                    // rows per set
+// sets per workgroup / workgroups per clip: bf16 4 / 2 (B = 256: 512
+// workgroups, one round at two per CU); f32 (the parity path, twice the
+// registers per operand) 1 / 8
+#ifndef PT_PB2_NSET
+#define PT_PB2_NSET 4
+#endif
+template <class S> constexpr int pb2_nset() { return sizeof(S) == 2 ? PT_PB2_NSET : 1; }
+template <class S> constexpr int pb2_wgpc() { return IMG / (4 * pb2_nset<S>()); }
+constexpr int PB2_NPX = PB2_SET * IMG;        // 128 pixels per set
+constexpr int PB2_NQ = 10;                    // per-channel sums
+static_assert(PB2_NW == 2 * PB2_SET, "one half row per wave and set");
+static_assert(IMG / 4 <= PW_PARTS && IMG / 4 <= BNB_WG_PER_CLIP, "slab / BN slots per clip");
+template <class S> constexpr int pb2_lds_bytes() {
+  return pb2_nset<S>() * PB2_NPX * 16 /*xs*/ + PB2_NW * prs_bytes<S>() /*transpose scratch*/ +
+         5 * stg_bytes<S, PB2_NPX>() /*weight-gradient operands*/ + PB2_NW * PB2_NQ * 32 * 4 /*sums*/ +
+         (PB2_NT / 64) * 64 * 8 /*group-sum scratch (fp64)*/ + 16 /*flag*/;
+}
+// slab slots of the 10 sums, in this order: q 0 / 1 are the BatchNorm
+// partial (sum dy, sum dy xhat), so threads 0..63 hold the values to publish
+__constant__ int kPb2Slot[PB2_NQ] = {SM_BN0B, SM_BN0W, SM_ALPHA, SM_MU, SM_GBI, SM_GBE,
+                                     SM_PW0, SM_PW1, SM_PW2, SM_PB};
+
+__device__ __forceinline__ f32x2 lsum8(const f32x8& v) {
+  return f32x2{v[0] + v[1] + v[2] + v[3], v[4] + v[5] + v[6] + v[7]};
+}
+__device__ __forceinline__ f32x8 rb8(bool on, f32x8 v) {
+  if (on)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = rbf(true, v[e]);
+  return v;
+}
+template <class S> struct Pb2In { f32x8 ginh, Iprev; PrPk<S> dep, gE, dIt, ci; };
+template <class S, int HG>
+__device__ __forceinline__ Pb2In<S> pb2_load(const CellArgs<S>& a, int t, size_t ro, int lane) {
+  const size_t fs = fr_off(1, a.B);
+  Pb2In<S> w;
+  w.Iprev = zero8();
+  if constexpr (HG) {
+    w.ginh = pr_load<S>(a.at + t * fs + ro, lane);                    // g_inh = att_t
+    if (t > 0) w.Iprev = pr_load<float>(a.I + (t - 1) * fs + ro, lane);
+  } else {
+    if (t == 0) w.ginh = zero8();
+    else if (a.no_inh) w.ginh = pr_load<float>(a.E + (t - 1) * fs + ro, lane);
+    else w.ginh = pr_load<float>(a.I + (t - 1) * fs + ro, lane);
+  }
+  w.dep = pr_load_pk<S>(a.dEp + ro, lane);
+  w.gE = pr_load_pk<S>(a.gE + t * fs + ro, lane);
+  w.dIt = pr_load_pk<S>(a.dIt + ro, lane);
+  w.ci = PrPk<S>{};
+  if (!a.no_inh) w.ci = pr_load_pk<S>(a.ci + t * fs + ro, lane);
+  return w;
+}
+
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (PT_ABL(a.ablate) & 512) return;
+  const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NSET = pb2_nset<S>(), WGPC = pb2_wgpc<S>();
+  const int b = blockIdx.x / WGPC, part = blockIdx.x % WGPC;
+  const int t = a.t, T = a.T, B = a.B;
+  const int y0 = part * PB2_SET * NSET;
+  const int px0 = (wave >> 1) * IMG + (wave & 1) * HR;       // first pixel of the half row in its set
+  float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
+  f32x4* xs = (f32x4*)smem;                                  // [2 sets][128 px]
+  char* p = smem + NSET * PB2_NPX * 16;
+  S* scr = (S*)(p + wave * prs_bytes<S>());
+  p += PB2_NW * prs_bytes<S>();
+  constexpr int SE = stg_bytes<S, PB2_NPX>() / (int)sizeof(S);
+  S* st_dep = (S*)p;
+  S* st_ginh = st_dep + SE;
+  S* st_gE = st_dep + 2 * SE;
+  S* st_dip = st_dep + 3 * SE;
+  S* st_xv = st_dep + 4 * SE;
+  float* wsum = (float*)(p + 5 * stg_bytes<S, PB2_NPX>());
+  double* gscr = (double*)(wsum + PB2_NW * PB2_NQ * 32);
+  int* flag = (int*)(gscr + (PB2_NT / 64) * 64);
+  const int gi = wave >> 1, mt = wave & 1;                  // this wave's weight-gradient tile row
+  const bool do_wg = !(a.no_inh && gi < 2) && !(PT_ABL(a.ablate) & 16);
+  PT_TR(a, PT_K_PW_BB, 0);
+
+  auto row_off = [&](int set) {
+    return clip_off(b) + ((size_t)(y0 + set * PB2_SET) * IMG + px0) * C;
+  };
+  // set 0's tiles first (their latency overlaps the x staging), then the
+  // old values of the slab's sums
+  const Pb2In<S> in = pb2_load<S, HG>(a, t, row_off(0), lane);
+  float* sp = slab_p + (2 + gi) * 1024 + (16 * mt + 4 * g4) * 32 + n;
+  float wold[2][4];
+  const int so = tid < PB2_NQ * 32 ? SLAB_G + kPb2Slot[tid >> 5] * 32 + (tid & 31) : 0;
+  const float sold = tid < PB2_NQ * 32 ? slab_p[so] : 0.f;
+  stage_x(a.x, a.xu8, xs, b, t, T, y0, PB2_SET * NSET, tid, PB2_NT, a.ntx, a.nty);
+  __syncthreads();
+  PT_TR(a, PT_K_PW_BB, 2);
+
+  f32x4 wacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+
+  // one set (inlined once per set); the next set's tiles are loaded once this
+  // set's element-wise temporaries are dead, before its barriers
+  Pb2In<S> in1;
+  auto set_body = [&](const int set, const Pb2In<S> in) {
+    // the lane index laundered per set: the per-lane parameters and addresses
+    // are formed in the set instead of living across both as invariants
+    int tl = tid;
+    if constexpr (NSET > 1) asm volatile("" : "+v"(tl));
+    const int lane = tl & 63, n = lane & 15, g4 = lane >> 4;
+    const size_t ro = row_off(set);
+    f32x2 sm[PB2_NQ];
+#pragma unroll
+    for (int q = 0; q < PB2_NQ; ++q) sm[q] = f32x2{0.f, 0.f};
+    const f32x4* xr = xs + set * PB2_NPX + px0 + 4 * g4;
+    // this lane's channels 2n, 2n + 1
+    float w0[2], w1[2], w2[2], bp[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = 2 * n + k;
+      w0[k] = a.wpre[c * 3 + 0]; w1[k] = a.wpre[c * 3 + 1]; w2[k] = a.wpre[c * 3 + 2]; bp[k] = a.bpre[c];
+    }
+    const f32x8 depf = pr_widen(in.dep);
+    const f32x8 ginh = in.ginh;
+    f32x8 Iprev = in.Iprev;
+    sm[5] += lsum8(depf);                                              // e-gate biases
+    pr_stage<S, PB2_NPX>(st_dep, depf, px0, lane);
+    pr_stage<S, PB2_NPX>(st_ginh, ginh, px0, lane);
+    pr_stage<S, PB2_NPX>(st_gE, pr_widen(in.gE), px0, lane);
+    const f32x8 dIt = pr_widen(in.dIt);
+    const PrA<S> pe = pr_to_a<S>(scr, rb8(RND_G(a), depf), lane);
+    {
+      const f32x8 dg = pr_mm<S>(pe, a.g16t[5], a.no_inh ? dIt : zero8(), lane);   // no_inh: I_t = gE_t
+      pr_store<S>(a.dgEp + ro, lane, rb8(RND_T(a), dg));
+    }
+    if (a.no_inh) {
+      const f32x8 dEn = pr_mm<S>(pe, a.g16t[4], pr_load<S>(a.dEn + ro, lane), lane);
+      pr_store<S>(a.dEn + ro, lane, dEn);
+    } else {
+      const float* bs = a.bnstat + (size_t)t * 128;
+      const f32x2 al = pr_par(a.alpha, lane), mu = pr_par(a.mu, lane);
+      const f32x2 bw0 = pr_par(a.bnw0, lane), bb0 = pr_par(a.bnb0, lane);
+      const f32x2 m0 = pr_par(bs, lane), rs0 = pr_par(bs + 32, lane);
+      const f32x2 gb2 = pr_par(a.gb[2], lane), gb3 = pr_par(a.gb[3], lane);
+      // stem (models/InT.py:212-213) of the lane's 4 pixels; z: nl'(pre-activation)
+      // (hGRU keeps the pre-activation and forms nl' at its use, as k_pw_bb)
+      f32x8 z, xv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 xin = xr[i];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const float zr = w0[k] * xin[0] + w1[k] * xin[1] + w2[k] * xin[2] + bp[k];
+          if constexpr (HG) {
+            z[4 * k + i] = zr;
+            xv[4 * k + i] = Act<ACT>::f(zr);
+          } else {
+            float f, d;
+            Act<ACT>::fd(zr, f, d);
+            xv[4 * k + i] = f;
+            z[4 * k + i] = d;
+          }
+        }
+      }
+      f32x8 gpre;
+      {
+        const PrA<S> ax = pr_to_a<S>(scr, rb8(RND_G(a), xv), lane);
+        const PrA<S> ai = pr_to_a<S>(scr, rb8(RND_G(a), ginh), lane);
+        gpre = pr_mm<S>(ax, a.g16f[2], zero8(), lane);
+        gpre = pr_mm<S>(ai, a.g16f[3], gpre, lane);
+      }
+      const f32x8 civ = pr_widen(in.ci);
+      f32x8 dIp, dip, dx, dci;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = e >> 2;
+        const float A0 = bw0[k] * rs0[k], B0 = bb0[k] - bw0[k] * rs0[k] * m0[k];   // BN0 affine folded
+        const float Ir = ginh[e], dIr = dIt[e];
+        const float Ip = HG ? Iprev[e] : Ir;               // I_{t-1} of the update (:166)
+        const float xi = (civ[e] - m0[k]) * rs0[k];
+        const float cn = A0 * civ[e] + B0;
+        const float u = al[k] * Ir + mu[k];
+        const float pp = cn * u;
+        float fp, dfp, ih, dfq;
+        Act<ACT>::fd(pp, fp, dfp);
+        const float q = xv[e] - fp;
+        Act<ACT>::fd(q, ih, dfq);
+        const float ig = sigm_b(gpre[e], sig_nb(gb2[k] + gb3[k]));
+        const float dih = dIr * ig;
+        dip[e] = dIr * (ih - Ip) * ig * (1.f - ig);
+        const float dq = dih * dfq;
+        const float dp = -dq * dfp;
+        const float du = dp * cn;
+        dci[e] = dp * u;
+        dx[e] = dq;
+        // InT: dI_{t-1} collects the update and the gated-inhibition terms;
+        // hGRU: the gated-inhibition terms go to att (dA, kept in dIp)
+        dIp[e] = HG ? du * al[k] : dIr * (1.f - ig) + du * al[k];
+        if constexpr (HG) Iprev[e] = dIr * (1.f - ig);
+        sm[2][k] += du * Ir;
+        sm[3][k] += du;
+        sm[4][k] += dip[e];
+        sm[0][k] += dci[e];
+        sm[1][k] += dci[e] * xi;
+      }
+      pr_store<S>(a.dcI + ro, lane, rb8(RND_T(a), dci));
+      pr_stage<S, PB2_NPX>(st_dip, dip, px0, lane);
+      pr_stage<S, PB2_NPX>(st_xv, xv, px0, lane);
+      const PrA<S> pd = pr_to_a<S>(scr, rb8(RND_G(a), dip), lane);
+      dx = pr_mm<S>(pd, a.g16t[2], dx, lane);
+      // stem backward of this share (models/InT.py:212-213): dz = dx nl'(z)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 xin = xr[i];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int e = 4 * k + i;
+          const float dz = dx[e] * (HG ? Act<ACT>::d(z[e]) : z[e]);
+          sm[6][k] += dz * xin[0];
+          sm[7][k] += dz * xin[1];
+          sm[8][k] += dz * xin[2];
+          sm[9][k] += dz;
+        }
+      }
+      dIp = pr_mm<S>(pd, a.g16t[3], dIp, lane);
+      dIp = pr_mm<S>(pe, a.g16t[4], dIp, lane);
+      if constexpr (HG) {
+        pr_store<S>(a.dAt + ro, lane, dIp);
+        pr_store<S>(a.GI + ro, lane, Iprev);
+      } else {
+        pr_store<S>(a.GI + ro, lane, rb8(RND_T(a), dIp));
+      }
+    }
+    if (set + 1 < NSET) in1 = pb2_load<S, HG>(a, t, row_off(set + 1), lane);
+    // this set's per-channel sums over the half row -> the wave's LDS slots
+#pragma unroll
+    for (int q = 0; q < PB2_NQ; ++q) {
+      f32x2 v = sm[q];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        v[k] += __shfl_xor(v[k], 16);
+        v[k] += __shfl_xor(v[k], 32);
+      }
+      f32x2* ws = (f32x2*)(wsum + (wave * PB2_NQ + q) * 32 + 2 * n);
+      if (lane < 16) *ws = set == 0 ? v : *ws + v;
+    }
+    __syncthreads();
+    if (do_wg) {
+      const S* D = gi < 2 ? st_dip : st_dep;
+      const S* X = gi == 0 ? st_xv : gi == 3 ? st_gE : st_ginh;
+      pr_wgrad_acc<S, PB2_NPX>(D, X, mt, wacc, lane);
+    }
+    if (set + 1 < NSET) __syncthreads();                  // the operand slots are reused
+  };
+  set_body(0, in);
+  if constexpr (NSET > 1) set_body(1, in1);
+  if constexpr (NSET > 2) set_body(2, in1);
+  if constexpr (NSET > 3) set_body(3, in1);
+  static_assert(NSET <= 4, "set bodies");
+  PT_TR(a, PT_K_PW_BB, 3);
+  if (do_wg) {                            // the gate tiles' old slab values
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wold[nt][i] = sp[i * 32 + 16 * nt];
+  }
+  // (the last set's barrier before its contraction published the sums)
+  PT_TR(a, PT_K_PW_BB, 4);
+  // sums over the 8 waves (wave order) -> slab; threads 0..63: the BatchNorm partial
+  const bool bn = !a.no_inh && !(PT_ABL(a.ablate) & 8);
+  const BnSlot bo = bnb_slot(a, t, 0, B * WGPC);
+  float bv = 0.f;
+  if (tid < PB2_NQ * 32) {
+    const int q = tid >> 5, c = tid & 31;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < PB2_NW; ++w) s += wsum[(w * PB2_NQ + q) * 32 + c];
+    bv = s;
+    if (!(PT_ABL(a.ablate) & 32)) slab_p[so] = sold + s;
+  }
+  if (do_wg) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sp[i * 32 + 16 * nt] = wold[nt][i] + wacc[nt][i];
+  }
+  PT_TR(a, PT_K_PW_BB, 5);
+  if (bn) bn_publish<PB2_NT, false>(bo, blockIdx.x, bv, tid, flag, gscr);
+  PT_TR(a, PT_K_PW_BB, 6);
+}
+
 
 // Band geometry by halo width PAD (k <= 7: 3, k > 7: 7): D rows per band (so
 // that the band buffers fit in LDS) and buffers (2 = double-buffered; f32 at
@@ -2533,6 +2844,8 @@ struct PrepArgs {
   S *wf_inh, *wf_exc, *wt_inh, *wt_exc;
   S* gf[6];
   S* gt[6];
+  S* g16f[6];     // 16x16 B-operand forms for k_pw_bb2 (pt_pr.h): [k 2][KS][64 lanes]
+  S* g16t[6];
   int rnd;        // diagnostic: weights rounded to bf16 (f32 path, bit 1048576)
 };
 
@@ -2542,7 +2855,7 @@ __global__ void k_prep(PrepArgs<S> p) {
   const int K = p.K, KK = K * K;
   const int nconv = KK * TT::KS * 64 * TT::EPL;   // == C*C*K*K
   const int ngate = TT::KS * 64 * TT::EPL;        // == C*C
-  const int total = 4 * nconv + 12 * ngate;
+  const int total = 4 * nconv + 24 * ngate;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     if (e < 4 * nconv) {
       const int which = e / nconv, r = e % nconv;
@@ -2555,6 +2868,25 @@ __global__ void k_prep(PrepArgs<S> p) {
         const float v = which < 2 ? W[(n * C + kc) * KK + tap] : W[(kc * C + n) * KK + (KK - 1 - tap)];
         dst[r] = (S)rbf(p.rnd, v);
       }
+    } else if (e >= 4 * nconv + 12 * ngate) {
+      // 16x16 forms: column n of output tile k is channel o = 2n + k; K index =
+      // bf16: 8 (lane >> 4) + j, f32 (step s): 4 s + (lane >> 4) (pt_pr.h pr_mm)
+      const int e2 = e - 4 * nconv - 12 * ngate;
+      const int gi = e2 / ngate, r = e2 % ngate;
+      const int gate = gi % 6, tr = gi / 6;
+      int lane, kk;
+      if constexpr (sizeof(S) == 2) {
+        const int j = r % 8;
+        lane = (r / 8) % 64;
+        kk = 8 * (lane >> 4) + j;
+      } else {
+        lane = r % 64;
+        kk = 4 * ((r / 64) % 8) + (lane >> 4);
+      }
+      const int o = 2 * (lane & 15) + r / 512;
+      const float* G = p.g[gate];
+      const float v = tr == 0 ? G[o * C + kk] : G[kk * C + o];
+      (tr == 0 ? p.g16f[gate] : p.g16t[gate])[r] = (S)rbf(p.rnd, v);
     } else {
       const int e2 = e - 4 * nconv;
       const int gi = e2 / ngate, r = e2 % ngate;
@@ -2871,7 +3203,7 @@ struct Plan {
   size_t es;          // element size of S
   size_t frame;       // elements per frame tensor (B*NPIX*C)
   // saved offsets
-  size_t o_E, o_I, o_Ic, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], o_pad, saved;
+  size_t o_E, o_I, o_Ic, o_gE, o_ci, o_ce, o_eg, o_at, o_bnstat, o_wf[4], o_g[12], o_g16[12], o_pad, saved;
   // workspace offsets
   size_t o_bnf_cnt, o_bnf_part, o_bnf_grp, o_bnb_cnt, o_bnb_part, o_bnb_grp;   // BnSlot storage
   size_t o_bnf_done, o_err;   // persistent forward: group-sum counters [T][2], give-up flag
@@ -2919,6 +3251,7 @@ Plan plan(const pt_cell_desc* d) {
   p.o_bnstat = o; o += al((size_t)p.T * 128 * 4);
   for (int i = 0; i < 4; ++i) { p.o_wf[i] = o; o += al((size_t)C * C * p.K * p.K * p.es); }
   for (int i = 0; i < 12; ++i) { p.o_g[i] = o; o += al((size_t)C * C * p.es); }
+  for (int i = 0; i < 12; ++i) { p.o_g16[i] = o; o += al((size_t)C * C * p.es); }
   p.Cu = d->channels;
   p.o_pad = o; o += p.Cu < C ? al(pad_layout(p.K * p.K).total * 4) : 0;
   p.saved = o;
@@ -2970,6 +3303,8 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   for (int i = 0; i < 6; ++i) {
     a.gf[i] = (const F*)(saved + p.o_g[i]);
     a.gt[i] = (const F*)(saved + p.o_g[6 + i]);
+    a.g16f[i] = (const typename CellArgs<S>::F16*)(saved + p.o_g16[i]);
+    a.g16t[i] = (const typename CellArgs<S>::F16*)(saved + p.o_g16[6 + i]);
   }
   a.E = (float*)(saved + p.o_E); a.I = (float*)(saved + p.o_I);
   a.Ic = p.es == 2 ? (S*)(saved + p.o_Ic) : (S*)(saved + p.o_I); a.gE = (S*)(saved + p.o_gE);
@@ -2999,16 +3334,17 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   } while (0)
 
 template <class K, class A>
-void launch_pw(K kern, dim3 grid, size_t lds, hipStream_t st, const A& a) {
-  hipLaunchKernelGGL(kern, grid, dim3(PW_NT), lds, st, a);
+void launch_pw(K kern, dim3 grid, size_t lds, hipStream_t st, const A& a, int nt = PW_NT) {
+  hipLaunchKernelGGL(kern, grid, dim3(nt), lds, st, a);
 }
 
 // (activation, cell) -> kernel instantiation
-#define PW_LAUNCH(kern, grid, lds)                                              \
-  (a.hgru ? (a.act ? launch_pw(kern<S, 1, 1>, grid, lds, st, a)                  \
-                   : launch_pw(kern<S, 0, 1>, grid, lds, st, a))                 \
-          : (a.act ? launch_pw(kern<S, 1, 0>, grid, lds, st, a)                  \
-                   : launch_pw(kern<S, 0, 0>, grid, lds, st, a)))
+#define PW_LAUNCH_NT(kern, grid, lds, nt)                                       \
+  (a.hgru ? (a.act ? launch_pw(kern<S, 1, 1>, grid, lds, st, a, nt)              \
+                   : launch_pw(kern<S, 0, 1>, grid, lds, st, a, nt))             \
+          : (a.act ? launch_pw(kern<S, 1, 0>, grid, lds, st, a, nt)              \
+                   : launch_pw(kern<S, 0, 0>, grid, lds, st, a, nt)))
+#define PW_LAUNCH(kern, grid, lds) PW_LAUNCH_NT(kern, grid, lds, PW_NT)
 
 
 // (activation, cell) -> fused kernel instantiation: grid = clips, CONV_NT threads
@@ -3050,6 +3386,10 @@ int set_lds_attrs() {
   SETLDS((k_pw_fb<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
   SETLDS((k_pw_bb<S, 1, 1>), (pwb_lds_bytes<S>()));
+  SETLDS((k_pw_bb2<S, 0, 0>), (pb2_lds_bytes<S>()));
+  SETLDS((k_pw_bb2<S, 0, 1>), (pb2_lds_bytes<S>()));
+  SETLDS((k_pw_bb2<S, 1, 0>), (pb2_lds_bytes<S>()));
+  SETLDS((k_pw_bb2<S, 1, 1>), (pb2_lds_bytes<S>()));
   SETLDS((k_fused_fa<S, 0, 0>), fused_lds_bytes<S>());
   SETLDS((k_fused_fa<S, 0, 1>), fused_lds_bytes<S>());
   SETLDS((k_fused_fa<S, 1, 0>), fused_lds_bytes<S>());
@@ -3130,6 +3470,12 @@ bool fused_env() {             // read per call: tests A/B the two paths in one 
   const char* e = getenv("PT_CELL_FUSED");
   return !(e && e[0] == '0');
 }
+// k_pw_bb2 (the half-row backward point-wise B, r04) by default;
+// PT_PWB2=0 (read per call) selects k_pw_bb.
+bool pwb2_env() {
+  const char* e = getenv("PT_PWB2");
+  return !(e && e[0] == '0');
+}
 bool use_fused(const pt_cell_desc* d, const Plan& p) {
   return fused_env() && d->dtype == PT_DTYPE_BF16 && p.ntx * p.nty == 1 &&
          p.K <= 2 * PADMAX + 1 && !d->no_inh;
@@ -3189,6 +3535,8 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
     pa.g[i] = pr->gate_w[i];
     pa.gf[i] = (S*)((char*)saved + p.o_g[i]);
     pa.gt[i] = (S*)((char*)saved + p.o_g[6 + i]);
+    pa.g16f[i] = (S*)((char*)saved + p.o_g16[i]);
+    pa.g16t[i] = (S*)((char*)saved + p.o_g16[6 + i]);
   }
   pa.wf_inh = (S*)((char*)saved + p.o_wf[0]); pa.wf_exc = (S*)((char*)saved + p.o_wf[1]);
   pa.wt_inh = (S*)((char*)saved + p.o_wf[2]); pa.wt_exc = (S*)((char*)saved + p.o_wf[3]);
@@ -3333,6 +3681,8 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   };
   // diagnostics only (env PT_CELL_DEBUG_STOP = n): return after the sweep's
   // first n launches, leaving the transients as that launch wrote them
+  const bool pwb2 = pwb2_env();
+  const int nprod_b = p.B * (pwb2 ? pb2_wgpc<S>() : PWB_WGPC);     // BN0 backward producers
   const int stop_at = debug_stop_env();
   int n_launch = 0;
   auto stop = [&] { return stop_at > 0 && ++n_launch >= stop_at; };
@@ -3352,15 +3702,18 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       launch_conv_bwd<S>(p, st, cb); });
     if (stop()) return 0;
     a.t = t;
-    timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
+    if (pwb2)
+      timed(PT_K_PW_BB, st, [&] { PW_LAUNCH_NT(k_pw_bb2, dim3(p.B * pb2_wgpc<S>()), (pb2_lds_bytes<S>()), PB2_NT); });
+    else
+      timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
     if (stop()) return 0;
     a.conv_done = 0;
     if (!d->no_inh) {
-      if (int rc = sync_bwd(t, 0, p.B * PWB_WGPC)) return rc;
+      if (int rc = sync_bwd(t, 0, nprod_b)) return rc;
       // dgE_t = conv^T(BN0-bwd(dcI), w_inh) + e_u^T d_e_pre ; frame 0's conv^T is dead (E_{-1}=0)
       ConvArgs<S> ca = conv_args(a);
       ca.dc = a.dcI; ca.raw = a.ci + t * fs; ca.bnstat = bst + (size_t)t * 128;
-      bwd_src(ca, t, 0, p.B * PWB_WGPC);
+      bwd_src(ca, t, 0, nprod_b);
       ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
       ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
       if (t >= 1) {
@@ -3480,7 +3833,7 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
       if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
       ptg::Key k;
       k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
-          .add(band_env());
+          .add(band_env()).add(pwb2_env());
       rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
     }
     if (rc) return rc;

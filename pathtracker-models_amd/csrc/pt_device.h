@@ -327,25 +327,28 @@ __device__ __forceinline__ float ftanh(float x) {
 // Compile-time activation (a runtime switch made the compiler branch around
 // every transcendental).  Branch-free: both sides are computed and selected.
 //   softplus: f = x > 20 ? x : log(1 + e^x);  f' = x > 20 ? 1 : e^x / (1 + e^x)
+//             (as max(log(1 + e^min(x, 20)), x) and e / (1 + e) at e = e^min(x, 20):
+//             the selects folded, r04; equal to within an ulp)
 //   tanh    : f = tanh x;                     f' = 1 - tanh^2 x
 template <int ACT> struct Act;
 template <> struct Act<0> {
   __device__ static __forceinline__ float f(float x) {
-    const float r = flog(1.f + fexp(fminf(x, 20.f)));
-    return x > 20.f ? x : r;
+    // log(1 + e^x) > x for every x, and at the clamp (x > 20) it is 20.0: the
+    // threshold select is a max
+    return fmaxf(flog(1.f + fexp(fminf(x, 20.f))), x);
   }
   __device__ static __forceinline__ float d(float x) {
+    // e / (1 + e) at the clamp (x > 20) is 1 to within an ulp: no select
     const float e = fexp(fminf(x, 20.f));
-    const float r = e * frcp(1.f + e);
-    return x > 20.f ? 1.f : r;
+    return e * frcp(1.f + e);
   }
   // f and f' from one exponential
   __device__ static __forceinline__ void fd(float x, float& f, float& d) {
     const float e = fexp(fminf(x, 20.f));
     const float s = 1.f + e;
     const float lf = flog(s), ld = e * frcp(s);
-    f = x > 20.f ? x : lf;
-    d = x > 20.f ? 1.f : ld;
+    f = fmaxf(lf, x);
+    d = ld;
   }
 };
 template <> struct Act<1> {
