@@ -2451,6 +2451,265 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
   PT_TR(a, PT_K_PW_BB, 6);
 }
 
+// =========================================================================
+// k_pw_ba2 (r04): backward point-wise A in the half-row PR layout (pt_pr.h),
+// the same arithmetic as k_pw_ba (models/InT.py:148-153 and :172-175
+// differentiated): tail = the attention backward of frame t + 1 and the stem
+// gradient; head = the excitation update backward of frame t.  Workgroup
+// structure as k_pw_bb2: 8 waves, one half row each per set of 4 rows, bf16
+// 4 sets (16 rows, 2 workgroups per clip: the same BatchNorm producer split
+// and slab partitions as k_pw_ba) / f32 1 set; after each set waves 0-3
+// contract the a_w / a_u weight-gradient tiles (D = d att_pre, X = x / E_t)
+// over the set's 128 pixels into registers.
+// =========================================================================
+constexpr int PA2_NQ = 9;
+template <class S> constexpr int pa2_nset() { return sizeof(S) == 2 ? 4 : 1; }
+template <class S> constexpr int pa2_wgpc() { return IMG / (4 * pa2_nset<S>()); }
+template <class S> constexpr int pa2_lds_bytes() {
+  return pa2_nset<S>() * PB2_NPX * 16 /*xs*/ + PB2_NW * prs_bytes<S>() /*transpose scratch*/ +
+         3 * stg_bytes<S, PB2_NPX>() /*weight-gradient operands*/ + PB2_NW * PA2_NQ * 32 * 4 /*sums*/ +
+         (PB2_NT / 64) * 64 * 8 /*group-sum scratch (fp64)*/ + 16 /*flag*/;
+}
+// slab slots of the 9 sums; q 0 / 1 = the BatchNorm partial (sum dy, sum dy xhat)
+__constant__ int kPa2Slot[PA2_NQ] = {SM_BN1B, SM_BN1W, SM_GBA, SM_KAPPA, SM_GAMMA,
+                                     SM_PW0, SM_PW1, SM_PW2, SM_PB};
+template <class S> struct Pa2In { PrPk<S> dgE, dAt, ce, eg, dEn; f32x8 Et, Iv, Eo; };
+
+template <class S, int ACT, int HG>
+__global__ __launch_bounds__(PB2_NT, 4) void k_pw_ba2(CellArgs<S> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (PT_ABL(a.ablate) & 512) return;
+  constexpr int NSET = pa2_nset<S>(), WGPC = pa2_wgpc<S>();
+  const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x / WGPC, part = blockIdx.x % WGPC;
+  const int t = a.t, T = a.T, B = a.B;
+  const int tt = t + 1;
+  const bool tail = tt <= T - 1, head = t >= 0;
+  const bool att_bwd = tail && (head || HG);      // InT at tt = 0 has none (gE_0 = att * E_{-1} = 0)
+  const int y0 = part * 4 * NSET;
+  const int px0 = (wave >> 1) * IMG + (wave & 1) * HR;
+  const size_t fs = fr_off(1, B);
+  float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
+  f32x4* xs = (f32x4*)smem;                                  // [NSET][128 px]
+  char* p = smem + NSET * PB2_NPX * 16;
+  S* scr = (S*)(p + wave * prs_bytes<S>());
+  p += PB2_NW * prs_bytes<S>();
+  constexpr int SE = stg_bytes<S, PB2_NPX>() / (int)sizeof(S);
+  S* st_dap = (S*)p;
+  S* st_xv = st_dap + SE;
+  S* st_E = st_dap + 2 * SE;
+  float* wsum = (float*)(p + 3 * stg_bytes<S, PB2_NPX>());
+  double* gscr = (double*)(wsum + PB2_NW * PA2_NQ * 32);
+  int* flag = (int*)(gscr + (PB2_NT / 64) * 64);
+  const int gi = wave >> 1, mt = wave & 1;                  // waves 0-3: a_w / a_u tile rows
+  const bool do_wg = att_bwd && wave < 4 && !(PT_ABL(a.ablate) & 16);
+  const S* dgsrc = a.conv_done ? a.dgE : a.dgEp;
+  PT_TR(a, PT_K_PW_BA, 0);
+
+  auto row_off = [&](int set) { return clip_off(b) + ((size_t)(y0 + set * 4) * IMG + px0) * C; };
+  auto tail_load = [&](int set, int ln) {
+    Pa2In<S> w;
+    const size_t ro = row_off(set);
+    w.dgE = PrPk<S>{};
+    w.dAt = PrPk<S>{};
+    w.Et = zero8();
+    if (att_bwd) {
+      if (head) {
+        w.dgE = pr_load_pk<S>(dgsrc + ro, ln);
+        w.Et = pr_load<float>(a.E + t * fs + ro, ln);
+      }
+      if constexpr (HG) w.dAt = pr_load_pk<S>(a.dAt + ro, ln);
+    }
+    w.Iv = zero8(); w.Eo = zero8();
+    w.ce = PrPk<S>{}; w.eg = PrPk<S>{}; w.dEn = PrPk<S>{};
+    if (head) {
+      w.Iv = pr_load<float>(a.I + t * fs + ro, ln);
+      w.ce = pr_load_pk<S>(a.ce + t * fs + ro, ln);
+      w.eg = pr_load_pk<S>(a.eg + t * fs + ro, ln);
+      if (t > 0) w.Eo = pr_load<float>(a.E + (t - 1) * fs + ro, ln);
+      if (tail) w.dEn = pr_load_pk<S>(a.dEn + ro, ln);
+    }
+    return w;
+  };
+  const Pa2In<S> in = tail_load(0, lane);
+  float* sp = slab_p + gi * 1024 + (16 * mt + 4 * g4) * 32 + n;     // slab gates 0 (a_w), 1 (a_u)
+  float wold[2][4];
+  const int so = tid < PA2_NQ * 32 ? SLAB_G + kPa2Slot[tid >> 5] * 32 + (tid & 31) : 0;
+  const float sold = tid < PA2_NQ * 32 ? slab_p[so] : 0.f;
+  if (tail) stage_x(a.x, a.xu8, xs, b, tt, T, y0, 4 * NSET, tid, PB2_NT, a.ntx, a.nty);
+  __syncthreads();
+  PT_TR(a, PT_K_PW_BA, 2);
+  f32x4 wacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  Pa2In<S> in1;
+
+  auto set_body = [&](const int set, const Pa2In<S> in) {
+    int tl = tid;
+    if constexpr (NSET > 1) asm volatile("" : "+v"(tl));
+    const int lane = tl & 63, n = lane & 15, g4 = lane >> 4;
+    const size_t ro = row_off(set);
+    const f32x8& Iv = in.Iv;
+    const f32x8& Eo = in.Eo;
+    f32x8 GE = zero8();
+    if (!tail) GE = pr_load<float>(a.GEfin + ro, lane);
+    f32x2 sm[PA2_NQ];
+#pragma unroll
+    for (int q = 0; q < PA2_NQ; ++q) sm[q] = f32x2{0.f, 0.f};
+    if (tail) {
+      const f32x4* xr = xs + set * PB2_NPX + px0 + 4 * g4;
+      float w0[2], w1[2], w2[2], bp[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = 2 * n + k;
+        w0[k] = a.wpre[c * 3 + 0]; w1[k] = a.wpre[c * 3 + 1]; w2[k] = a.wpre[c * 3 + 2]; bp[k] = a.bpre[c];
+      }
+      f32x8 z, xv;                           // z: nl'(stem pre-activation)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 xin = xr[i];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const float zr = w0[k] * xin[0] + w1[k] * xin[1] + w2[k] * xin[2] + bp[k];
+          float f, d;
+          Act<ACT>::fd(zr, f, d);
+          xv[4 * k + i] = f;
+          z[4 * k + i] = d;
+        }
+      }
+      // this kernel's share of d xbn_tt (a_w^T d_att_pre); k_pw_bb adds the
+      // inhibition path's share to the same stem-gradient sums itself
+      f32x8 dx = zero8();
+      if (head || HG) {
+        const f32x8 dgE = pr_widen(in.dgE);
+        const f32x8 dAt = pr_widen(in.dAt);
+        const f32x8& Et = in.Et;
+        const f32x2 gb0 = pr_par(a.gb[0], lane), gb1 = pr_par(a.gb[1], lane);
+        f32x8 gpre;
+        {
+          const PrA<S> ax = pr_to_a<S>(scr, rb8(RND_G(a), xv), lane);
+          const PrA<S> ae = pr_to_a<S>(scr, rb8(RND_G(a), Et), lane);
+          gpre = pr_mm<S>(ax, a.g16f[0], zero8(), lane);
+          gpre = pr_mm<S>(ae, a.g16f[1], gpre, lane);
+        }
+        f32x8 att, dap;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = e >> 2;
+          att[e] = sigm_b(gpre[e], sig_nb(gb0[k] + gb1[k]));
+          const float datt = HG ? dgE[e] * Et[e] + dAt[e] : dgE[e] * Et[e];
+          dap[e] = datt * att[e] * (1.f - att[e]);
+          sm[2][k] += dap[e];
+        }
+        pr_stage<S, PB2_NPX>(st_dap, dap, px0, lane);
+        pr_stage<S, PB2_NPX>(st_xv, xv, px0, lane);
+        pr_stage<S, PB2_NPX>(st_E, Et, px0, lane);
+        const PrA<S> pd = pr_to_a<S>(scr, rb8(RND_G(a), dap), lane);
+        if (head) {
+          const f32x8 dEn = pr_widen(in.dEn);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) GE[e] = dEn[e] + dgE[e] * att[e];
+          GE = pr_mm<S>(pd, a.g16t[1], GE, lane);
+        }
+        dx = pr_mm<S>(pd, a.g16t[0], dx, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 xin = xr[i];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const float dz = dx[4 * k + i] * z[4 * k + i];
+          sm[5][k] += dz * xin[0];
+          sm[6][k] += dz * xin[1];
+          sm[7][k] += dz * xin[2];
+          sm[8][k] += dz;
+        }
+      }
+    }
+    if (head) {
+      const float* bst = a.bnstat + (size_t)t * 128;
+      const f32x2 m1 = pr_par(bst + 64, lane), rs1 = pr_par(bst + 96, lane);
+      const f32x2 kap = pr_par(a.kappa, lane), gam = pr_par(a.gamma, lane);
+      const f32x2 bw1 = pr_par(a.bnw1, lane), bb1 = pr_par(a.bnb1, lane);
+      const f32x8 cev = pr_widen(in.ce), egv = pr_widen(in.eg);
+      f32x8 dIl, dEn, dEp, dcE;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = e >> 2;
+        const float xe = (cev[e] - m1[k]) * rs1[k];
+        const float cn = bw1[k] * xe + bb1[k];
+        const float w = kap[k] * Iv[e] + gam[k];
+        const float pe = cn * w;
+        float eh, ehd;
+        Act<ACT>::fd(pe, eh, ehd);
+        const float deg = GE[e] * (eh - Eo[e]);
+        const float dpe = GE[e] * egv[e] * ehd;
+        const float dce = dpe * w;
+        const float dw = dpe * cn;
+        sm[3][k] += dw * Iv[e];
+        sm[4][k] += dw;
+        dIl[e] = dw * kap[k];
+        dEn[e] = (1.f - egv[e]) * GE[e];
+        dEp[e] = deg * egv[e] * (1.f - egv[e]);
+        dcE[e] = dce;
+        sm[0][k] += dce;
+        sm[1][k] += dce * xe;
+      }
+      pr_store<S>(a.dIl + ro, lane, rb8(RND_T(a), dIl));
+      pr_store<S>(a.dEn + ro, lane, rb8(RND_T(a), dEn));
+      pr_store<S>(a.dEp + ro, lane, rb8(RND_T(a), dEp));
+      pr_store<S>(a.dcE + ro, lane, rb8(RND_T(a), dcE));
+    }
+    if (set + 1 < NSET) in1 = tail_load(set + 1, lane);
+#pragma unroll
+    for (int q = 0; q < PA2_NQ; ++q) {
+      f32x2 v = sm[q];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        v[k] += __shfl_xor(v[k], 16);
+        v[k] += __shfl_xor(v[k], 32);
+      }
+      f32x2* ws = (f32x2*)(wsum + (wave * PA2_NQ + q) * 32 + 2 * n);
+      if (lane < 16) *ws = set == 0 ? v : *ws + v;
+    }
+    __syncthreads();
+    if (do_wg) pr_wgrad_acc<S, PB2_NPX>(st_dap, gi == 0 ? st_xv : st_E, mt, wacc, lane);
+    if (set + 1 < NSET) __syncthreads();                  // the operand slots are reused
+  };
+  set_body(0, in);
+  if constexpr (NSET > 1) set_body(1, in1);
+  if constexpr (NSET > 2) set_body(2, in1);
+  if constexpr (NSET > 3) set_body(3, in1);
+  static_assert(NSET <= 4, "set bodies");
+  PT_TR(a, PT_K_PW_BA, 3);
+  if (do_wg) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wold[nt][i] = sp[i * 32 + 16 * nt];
+  }
+  PT_TR(a, PT_K_PW_BA, 4);
+  const bool bn = head && !(PT_ABL(a.ablate) & 8);
+  const BnSlot bo = bnb_slot(a, t, 1, B * WGPC);
+  float bv = 0.f;
+  if (tid < PA2_NQ * 32) {
+    const int q = tid >> 5, c = tid & 31;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < PB2_NW; ++w) s += wsum[(w * PA2_NQ + q) * 32 + c];
+    bv = s;
+    if (!(PT_ABL(a.ablate) & 32)) slab_p[so] = sold + s;
+  }
+  if (do_wg) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sp[i * 32 + 16 * nt] = wold[nt][i] + wacc[nt][i];
+  }
+  PT_TR(a, PT_K_PW_BA, 5);
+  if (bn) bn_publish<PB2_NT, false>(bo, blockIdx.x, bv, tid, flag, gscr);
+  PT_TR(a, PT_K_PW_BA, 6);
+}
+
 
 // Band geometry by halo width PAD (k <= 7: 3, k > 7: 7): D rows per band (so
 // that the band buffers fit in LDS) and buffers (2 = double-buffered; f32 at
@@ -3390,6 +3649,10 @@ int set_lds_attrs() {
   SETLDS((k_pw_bb2<S, 0, 1>), (pb2_lds_bytes<S>()));
   SETLDS((k_pw_bb2<S, 1, 0>), (pb2_lds_bytes<S>()));
   SETLDS((k_pw_bb2<S, 1, 1>), (pb2_lds_bytes<S>()));
+  SETLDS((k_pw_ba2<S, 0, 0>), (pa2_lds_bytes<S>()));
+  SETLDS((k_pw_ba2<S, 0, 1>), (pa2_lds_bytes<S>()));
+  SETLDS((k_pw_ba2<S, 1, 0>), (pa2_lds_bytes<S>()));
+  SETLDS((k_pw_ba2<S, 1, 1>), (pa2_lds_bytes<S>()));
   SETLDS((k_fused_fa<S, 0, 0>), fused_lds_bytes<S>());
   SETLDS((k_fused_fa<S, 0, 1>), fused_lds_bytes<S>());
   SETLDS((k_fused_fa<S, 1, 0>), fused_lds_bytes<S>());
@@ -3475,6 +3738,14 @@ bool fused_env() {             // read per call: tests A/B the two paths in one 
 bool pwb2_env() {
   const char* e = getenv("PT_PWB2");
   return !(e && e[0] == '0');
+}
+// k_pw_ba2 (its PR-layout counterpart): opt-in (PT_PWA2=1).  Measured r04
+// (B=256 T=64, interleaved): 59.9-60.1 vs 58.4-58.7 us for k_pw_ba, which
+// already ran one round of workgroups (4 rows per wave); k_pw_bb2's gain came
+// from halving the rounds, not from the layout.
+bool pwa2_env() {
+  const char* e = getenv("PT_PWA2");
+  return e && e[0] == '1';
 }
 bool use_fused(const pt_cell_desc* d, const Plan& p) {
   return fused_env() && d->dtype == PT_DTYPE_BF16 && p.ntx * p.nty == 1 &&
@@ -3681,21 +3952,28 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   };
   // diagnostics only (env PT_CELL_DEBUG_STOP = n): return after the sweep's
   // first n launches, leaving the transients as that launch wrote them
-  const bool pwb2 = pwb2_env();
+  const bool pwb2 = pwb2_env(), pwa2 = pwa2_env();
   const int nprod_b = p.B * (pwb2 ? pb2_wgpc<S>() : PWB_WGPC);     // BN0 backward producers
+  const int nprod_a = p.B * (pwa2 ? pa2_wgpc<S>() : PWA_WGPC);     // BN1 backward producers
+  auto launch_pwa = [&] {
+    if (pwa2)
+      timed(PT_K_PW_BA, st, [&] { PW_LAUNCH_NT(k_pw_ba2, dim3(nprod_a), (pa2_lds_bytes<S>()), PB2_NT); });
+    else
+      timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+  };
   const int stop_at = debug_stop_env();
   int n_launch = 0;
   auto stop = [&] { return stop_at > 0 && ++n_launch >= stop_at; };
   a.t = p.T - 1;
   a.conv_done = 0;
-  timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+  launch_pwa();
   if (stop()) return 0;
-  if (int rc = sync_bwd(p.T - 1, 1, p.B * PWA_WGPC)) return rc;
+  if (int rc = sync_bwd(p.T - 1, 1, nprod_a)) return rc;
   for (int t = p.T - 1; t >= 0; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
     cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
-    bwd_src(cb, t, 1, p.B * PWA_WGPC);
+    bwd_src(cb, t, 1, nprod_a);
     cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
     cb.wf = a.wt_exc; cb.out = a.dIt; cb.add0 = a.dIl; cb.add1 = t < p.T - 1 && !d->no_inh ? a.GI : nullptr;
     timed(PT_K_CONV_BB, st, [&] {
@@ -3727,10 +4005,10 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       if (stop()) return 0;
     }
     a.t = t - 1;
-    timed(PT_K_PW_BA, st, [&] { PW_LAUNCH(k_pw_ba, gpa, lpa); });
+    launch_pwa();
     if (stop()) return 0;
     if (t >= 1)
-      if (int rc = sync_bwd(t - 1, 1, p.B * PWA_WGPC)) return rc;
+      if (int rc = sync_bwd(t - 1, 1, nprod_a)) return rc;
   }
   r.part = 0;
   timed(PT_K_REDUCE, st, [&] {
@@ -3833,7 +4111,7 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
       if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
       ptg::Key k;
       k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
-          .add(band_env()).add(pwb2_env());
+          .add(band_env()).add(pwb2_env()).add(pwa2_env());
       rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
     }
     if (rc) return rc;

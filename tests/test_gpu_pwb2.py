@@ -1,5 +1,6 @@
-"""k_pw_bb2 (the half-row backward point-wise B, r04, pt_pr.h) against the
-CL-layout k_pw_bb it replaces (PT_PWB2=0), in one process: every parameter
+"""k_pw_bb2 / k_pw_ba2 (the half-row backward point-wise kernels, r04, pt_pr.h)
+against the CL-layout k_pw_bb / k_pw_ba they replace (PT_PWB2=0 PT_PWA2=0), in
+one process: every parameter
 gradient of one forward + backward, f32 (different summation order only:
 1e-5 relative) and bf16 (its own rounding of the 1x1 gate and weight-gradient
 operands: gradient cosine), for InT, InT no_inh and hGRU.  The reference
@@ -46,17 +47,21 @@ def test_pwb2_matches_pwb(kind, dtype):
     m = m.to(dev)
     m.cell_dtype = dtype
     x, y = bench.make_data(77, 24, t, dev)
-    old = os.environ.get("PT_PWB2")
+    keys = ("PT_PWB2", "PT_PWA2")
+    old = {k: os.environ.get(k) for k in keys}
     try:
-        os.environ["PT_PWB2"] = "0"
+        for k in keys:
+            os.environ[k] = "0"
         g0 = _grads(m, x, y)
-        os.environ["PT_PWB2"] = "1"
+        for k in keys:
+            os.environ[k] = "1"
         g1 = _grads(m, x, y)
     finally:
-        if old is None:
-            os.environ.pop("PT_PWB2", None)
-        else:
-            os.environ["PT_PWB2"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     assert g0.keys() == g1.keys()
     for k in g0:
         a, b = g1[k], g0[k]
