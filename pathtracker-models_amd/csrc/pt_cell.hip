@@ -471,7 +471,18 @@ struct CellArgs {
   int bn_world;                         // replicas sharing the statistics (1 = per replica)
   float* slab;                          // [B][PW_PARTS][SLAB]
   int conv_done;                        // k_pw_ba: dgE holds conv^T(w_inh) + dgEp
+  int xmap;                             // XCD-affine workgroup order (wg_split)
 };
+
+// Workgroup j of a launch with nper workgroups per clip -> (clip b, part).
+// xmap (default, PT_XCD_MAP != 0): b = j % B, part = j / B, so that every
+// kernel of a step places clip b on the same XCD (workgroups go to XCDs
+// round-robin, j % 8; B a multiple of 8) and a clip's tensors written by one
+// launch are read by the next one from the same XCD's L2; else b = j / nper.
+__device__ __forceinline__ void wg_split(int j, int nper, int B, int xmap, int& b, int& part) {
+  if (xmap) { b = j % B; part = j / B; }
+  else { b = j / nper; part = j % nper; }
+}
 
 // Phase stamp (diagnostics, pt_cell_trace): thread 0 of every (gridDim.x / 256)-th
 // workgroup of the traced frame writes the 100 MHz real-time counter into slot
@@ -780,6 +791,7 @@ struct ConvArgs {
   using F = typename Tr<S>::frag;
   int B, K, ablate;
   int ntx, nty;                 // tiles per frame (halo from neighbours when > 1 x 1)
+  int xmap;                     // XCD-affine workgroup order (wg_split)
   const S* src;                 // FILL_COPY: frame base [B][NPIX][C]
   const S* dc;                  // FILL_BNBWD: dy
   const S* raw;                 // FILL_BNBWD: pre-BN conv output of the forward
@@ -1061,7 +1073,9 @@ __global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a
   float* tbl = (float*)(smem + band_tile_bytes());
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, px = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x >> 1, y0 = (blockIdx.x & 1) * BAND_ROWS;
+  int b, band;
+  wg_split(blockIdx.x, 2, a.B, a.xmap, b, band);
+  const int y0 = band * BAND_ROWS;
   const size_t cb = clip_off(b);
   if (tid < 32) {     // BN backward as an affine map per channel (as conv_body)
     const double inv = 1.0 / ((double)a.bnB * NPIX);
@@ -1483,7 +1497,8 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fa(CellArgs<S> a) {
   const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
+  int b, part;
+  wg_split(blockIdx.x, PWF_WGPC, a.B, a.xmap, b, part);
   const int t = a.t, T = a.T, B = a.B;
   const int y0 = part * PW_NW;
   const int yl = wave, y = y0 + yl;
@@ -1569,7 +1584,8 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
   const PLds L = pcarve<PWF_RPP>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x / PWF_WGPC, part = blockIdx.x % PWF_WGPC;
+  int b, part;
+  wg_split(blockIdx.x, PWF_WGPC, a.B, a.xmap, b, part);
   const int t = a.t, T = a.T, B = a.B;
   const int y0 = part * PW_NW;
   const int yl = wave, y = y0 + yl;
@@ -1668,7 +1684,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
                          b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   // this wave's first row's tiles go out before the staging and the barrier
   FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
-  tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
+  tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
   PT_TR(a, PT_K_FUSED_FA, 2);
@@ -1703,7 +1719,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
                          b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
   FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
-  tile_zero<S, PADMAX, CONV_NT>((S*)L.tile, tid);
+  tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   __syncthreads();
   PT_TR(a, PT_K_FUSED_FB, 2);
@@ -1919,7 +1935,9 @@ template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (PT_ABL(a.ablate) & 512) return;
-  pw_ba_body<S, ACT, HG, PWA_RPP>(a, smem, blockIdx.x / PWA_WGPC, blockIdx.x % PWA_WGPC);
+  int b, part;
+  wg_split(blockIdx.x, PWA_WGPC, a.B, a.xmap, b, part);
+  pw_ba_body<S, ACT, HG, PWA_RPP>(a, smem, b, part);
 }
 
 // -------------------------------------------------------------------------
@@ -2141,7 +2159,9 @@ template <class S, int ACT, int HG>
 __global__ __launch_bounds__(PW_NT, 2) void k_pw_bb(CellArgs<S> a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (PT_ABL(a.ablate) & 512) return;
-  pw_bb_body<S, ACT, HG, PWB_RPP>(a, smem, blockIdx.x / PWB_WGPC, blockIdx.x % PWB_WGPC);
+  int b, part;
+  wg_split(blockIdx.x, PWB_WGPC, a.B, a.xmap, b, part);
+  pw_bb_body<S, ACT, HG, PWB_RPP>(a, smem, b, part);
 }
 
 // =========================================================================
@@ -2223,7 +2243,8 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
   const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NSET = pb2_nset<S>(), WGPC = pb2_wgpc<S>();
-  const int b = blockIdx.x / WGPC, part = blockIdx.x % WGPC;
+  int b, part;
+  wg_split(blockIdx.x, WGPC, a.B, a.xmap, b, part);
   const int t = a.t, T = a.T, B = a.B;
   const int y0 = part * PB2_SET * NSET;
   const int px0 = (wave >> 1) * IMG + (wave & 1) * HR;       // first pixel of the half row in its set
@@ -2255,6 +2276,7 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
   float wold[2][4];
   const int so = tid < PB2_NQ * 32 ? SLAB_G + kPb2Slot[tid >> 5] * 32 + (tid & 31) : 0;
   const float sold = tid < PB2_NQ * 32 ? slab_p[so] : 0.f;
+  PT_TR(a, PT_K_PW_BB, 1);
   stage_x(a.x, a.xu8, xs, b, t, T, y0, PB2_SET * NSET, tid, PB2_NT, a.ntx, a.nty);
   __syncthreads();
   PT_TR(a, PT_K_PW_BB, 2);
@@ -2482,7 +2504,8 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_ba2(CellArgs<S> a) {
   constexpr int NSET = pa2_nset<S>(), WGPC = pa2_wgpc<S>();
   const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x / WGPC, part = blockIdx.x % WGPC;
+  int b, part;
+  wg_split(blockIdx.x, WGPC, a.B, a.xmap, b, part);
   const int t = a.t, T = a.T, B = a.B;
   const int tt = t + 1;
   const bool tail = tt <= T - 1, head = t >= 0;
@@ -3452,6 +3475,12 @@ int debug_stop_env() {
 #endif
 }
 
+// PT_XCD_MAP=0 (read per call) selects the clip-major workgroup order (wg_split)
+int xmap_env() {
+  const char* e = getenv("PT_XCD_MAP");
+  return !(e && e[0] == '0');
+}
+
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
@@ -3548,6 +3577,7 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
   a.ntx = p.ntx; a.nty = p.nty;
   a.hgru = d->cell == PT_CELL_HGRU;
   a.bn_world = 1;
+  a.xmap = xmap_env();
   a.trace = g_trace;
   a.trace_t = g_trace_t;
   a.x = x;
@@ -3712,6 +3742,7 @@ ConvArgs<S> conv_args(const CellArgs<S>& a) {
   c.B = a.B; c.K = a.K; c.ablate = a.ablate;
   c.bnB = a.B * a.bn_world;
   c.ntx = a.ntx; c.nty = a.nty;
+  c.xmap = a.xmap;
   return c;
 }
 
@@ -4068,7 +4099,7 @@ int pt_cell_forward_dist(const pt_cell_desc* d, const void* x, const pt_cell_par
   ptg::Key k;
   k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env())
       .add(fused_env())
-      .add(persist_env());
+      .add(persist_env()).add(xmap_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }
 
@@ -4111,7 +4142,7 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
       if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
       ptg::Key k;
       k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
-          .add(band_env()).add(pwb2_env()).add(pwa2_env());
+          .add(band_env()).add(pwb2_env()).add(pwa2_env()).add(xmap_env());
       rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
     }
     if (rc) return rc;

@@ -466,6 +466,21 @@ __device__ void tile_zero(S* tile, int tid) {
   for (int i = tid; i < n; i += NTH) p[i] = make_uint4(0, 0, 0, 0);
 }
 
+// Zero only the halo ring of the tile (the fused forward writes every interior
+// pixel before its conv reads the tile): 420 of 1444 pixels at PAD 3.
+template <class S, int PAD = PADMAX, int NTH = NT>
+__device__ void tile_zero_halo(S* tile, int tid) {
+  constexpr int TW = tile_w<PAD>(), PXB = Tr<S>::CP * (int)sizeof(S), CPP = PXB / 16;  // 16-B chunks per pixel
+  constexpr int NH = 2 * PAD * TW + 2 * PAD * IMG;
+  for (int i = tid; i < NH * CPP; i += NTH) {
+    const int hp = i / CPP, q = i - hp * CPP;
+    int r, c;
+    if (hp < 2 * PAD * TW) { const int j = hp / TW; r = j < PAD ? j : IMG + j; c = hp - j * TW; }
+    else { const int k = hp - 2 * PAD * TW, j = k / (2 * PAD); r = PAD + j; const int m = k - j * 2 * PAD; c = m < PAD ? m : IMG + m; }
+    *(uint4*)((char*)tile + (r * TW + c) * PXB + q * 16) = make_uint4(0, 0, 0, 0);
+  }
+}
+
 // Fill the tile interior with channels [pass*CP, pass*CP+CP) of a
 // channels-last clip image (global, [32][32][32] of S).  All 16 loads of a
 // thread are issued before any LDS store so one memory round trip covers the
