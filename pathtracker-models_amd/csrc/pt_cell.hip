@@ -2189,8 +2189,11 @@ constexpr int PB2_SET = 4;                    // rows per set
 #ifndef PT_PB2_NSET
 #define PT_PB2_NSET 4
 #endif
-template <class S> constexpr int pb2_nset() { return sizeof(S) == 2 ? PT_PB2_NSET : 1; }
-template <class S> constexpr int pb2_wgpc() { return IMG / (4 * pb2_nset<S>()); }
+// (hGRU, bf16: 2 sets -- its extra I_{t-1} tile spilled 33 VGPRs at 4)
+template <class S, int HG = 0> constexpr int pb2_nset() {
+  return sizeof(S) == 2 ? (HG ? 2 : PT_PB2_NSET) : 1;
+}
+template <class S, int HG = 0> constexpr int pb2_wgpc() { return IMG / (4 * pb2_nset<S, HG>()); }
 constexpr int PB2_NPX = PB2_SET * IMG;        // 128 pixels per set
 constexpr int PB2_NQ = 10;                    // per-channel sums
 static_assert(PB2_NW == 2 * PB2_SET, "one half row per wave and set");
@@ -2242,7 +2245,7 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
   if (PT_ABL(a.ablate) & 512) return;
   const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int NSET = pb2_nset<S>(), WGPC = pb2_wgpc<S>();
+  constexpr int NSET = pb2_nset<S, HG>(), WGPC = pb2_wgpc<S, HG>();
   int b, part;
   wg_split(blockIdx.x, WGPC, a.B, a.xmap, b, part);
   const int t = a.t, T = a.T, B = a.B;
@@ -3011,7 +3014,7 @@ __global__ __launch_bounds__((wgrad_nt<S, PAD>()), 1) void k_wgrad(CellArgs<S> a
   constexpr int NKW = NTH == WG8_NT ? 1 : 2;        // kernel columns per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   S* buf = (S*)smem;
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = blockIdx.x, conv = blockIdx.y + conv0, grp = blockIdx.z;
   const int KK = a.K * a.K;
@@ -3019,7 +3022,6 @@ __global__ __launch_bounds__((wgrad_nt<S, PAD>()), 1) void k_wgrad(CellArgs<S> a
   const S* Ds = conv == 0 ? a.dci_s : a.dce_s;
 
   float* dst = wslab + ((size_t)conv * nwg + g) * KK * 1024;
-  const int n = lane & 31;
   if constexpr (sizeof(S) == 2) {
     f32x16 acc[WG2_NACC];
 #pragma unroll
@@ -3060,7 +3062,7 @@ __global__ __launch_bounds__((wgrad_nt<S, PAD>()), 1) void k_wgrad(CellArgs<S> a
       const int kh = kh0 + m % 7, kw = kw0 + m / 7;
       if (kh < a.K && kw < a.K) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dst[(kh * a.K + kw) * 1024 + n * 32 + cl_x(r, h)] = acc[m][r];
+        for (int r = 0; r < 16; ++r) dst[(kh * a.K + kw) * 1024 + r * 64 + lane] = acc[m][r];
       }
     }
   } else {
@@ -3106,10 +3108,186 @@ __global__ __launch_bounds__((wgrad_nt<S, PAD>()), 1) void k_wgrad(CellArgs<S> a
       const int tap = tap0 + wave + 4 * m;
       if (tap < KK) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dst[tap * 1024 + n * 32 + cl_x(r, h)] = acc[m][r];
+        for (int r = 0; r < 16; ++r) dst[tap * 1024 + r * 64 + lane] = acc[m][r];
       }
     }
   }
+}
+
+// -------------------------------------------------------------------------
+// bf16, k = 7, 16 waves (r04, default; PT_WG16=0 selects the 8-wave form).
+// The 8-wave form gives wave w kernel column w (7 tiles): SIMD s runs waves s
+// and s + 4, so SIMDs 0-2 carry 14 tiles and SIMD 3 seven (wave 7 only
+// stages) -- 87.5 % of the MFMA rate at best, and two waves per SIMD hide
+// little.  Here the 49 tiles are (column, kernel rows 0-3) and (column,
+// kernel rows 4-6) units on 14 of 16 waves, placed so that the SIMDs carry
+// 13 / 12 / 12 / 12 tiles (wave w on SIMD w & 3): four waves per SIMD at
+// <= 128 VGPRs.  Per band and pixel block the wave streams the X rows of its
+// kernel rows once (one A fragment per X row, reused over its 3-4 taps) and
+// keeps a 5-row window of D fragments (one read ahead) instead of all 8.
+// -------------------------------------------------------------------------
+constexpr int WG16_NT = 1024;
+constexpr unsigned WG16_BIG = 0x0CCDu;                    // waves with kernel rows 0-3
+constexpr unsigned long long WG16_KW = 0xFF65654343212100ull;   // nibble w: column (15: stager)
+template <int KH0, int NKH>
+__device__ __forceinline__ void wgrad_band16(f32x16 (&acc)[4], const bf16_t* xt, const bf16_t* dt,
+                                             int kw, int lane) {
+  constexpr int PAD = PADMAX, off = PAD - 3;
+  constexpr int RB = wg_rb<bf16_t, PAD>();
+  constexpr int ns = RB + NKH - 1;                 // X rows of the unit
+  const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
+  const int chb = 16 * (grp & 1) + 4 * pp;
+  const int hh = grp >> 1;
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const bf16_t* xb = xt + wx_off<PAD>(off + KH0, blk * 16 + 8 * hh + q + off + kw, chb);
+    const bf16_t* db = dt + wd_off(0, blk * 16 + 8 * hh + q, chb);
+    bf16x8 dw[5], av[2];
+    dw[0] = tr_read8(db);
+    av[0] = tr_read8(xb);
+#pragma unroll
+    for (int s = 0; s < ns; ++s) {
+      const int cur = s & 1;
+      // one step ahead: X row s + 1 of this unit, D row s + 1 of the band
+      if (s + 1 < ns) av[cur ^ 1] = tr_read8(xb + (s + 1) * tile_w<PAD>() * C);
+      if (s + 1 < RB) dw[(s + 1) % 5] = tr_read8(db + (s + 1) * IMG * C);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NKH; ++j) {              // tap (KH0 + j, kw) pairs X row s with D row s - j
+        if (s - j >= 0 && s - j < RB) acc[j] = Tr<bf16_t>::mma(av[cur], dw[(s - j) % 5], acc[j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// LDS-DMA band staging (untiled frames): three band buffers; band u + 2's rows
+// are copied global -> LDS (global_load_lds_dwordx4, 1 KiB per wave-instruction,
+// lane-linear: one half interior row) while band u's MFMAs run, and a counted
+// vmcnt retires band u + 1 before a raw barrier.  With register staging
+// (wgrad_run) the band loads and the MFMAs measured additive
+// (profiles/r04_wgrad_ablate.txt).  44 chunks per band (28 X, 16 D), issued
+// by the two stager waves (below).
+constexpr int WG16_DMA_BUFS = 3;
+constexpr int wgrad16_dma_lds_bytes() {
+  return WG16_DMA_BUFS * wgrad_band_elems<bf16_t, PADMAX>() * 2 + 1024;
+}
+template <class Body>
+__device__ __forceinline__ void wgrad_run_dma(Body&& body, const bf16_t* __restrict__ Xs,
+                                              const bf16_t* __restrict__ Ds, int B, int T, int g, int nwg,
+                                              bf16_t* buf, int tid, int wave, int lane, int ablate) {
+  constexpr int PAD = PADMAX;
+  constexpr int BE = wgrad_band_elems<bf16_t, PAD>();
+  constexpr int RB = wg_rb<bf16_t, PAD>(), XR = wg_xr<bf16_t, PAD>(), NB = IMG / RB;
+  constexpr int XE = XR * tile_w<PAD>() * C;
+  const int npairs = (B * T - g + nwg - 1) / nwg;
+  const int nunits = npairs * NB;
+  for (int i = tid; i < WG16_DMA_BUFS * BE * 2 / 16; i += WG16_NT) ((u32x4*)buf)[i] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  // The DMAs are inline asm: the compiler's own LDS-DMA bookkeeping waits
+  // vmcnt(0) before every global_load_lds (it cannot tell the destinations
+  // apart), which would serialise them.  Addresses are wave-uniform (SGPR base,
+  // M0 = LDS byte offset) plus the lane's 16 B.
+  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) bf16_t*)buf;
+  const unsigned voff = lane * 16;
+  auto dma = [&](const bf16_t* src, unsigned ldst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(src), "s"(ldst) : "memory");
+  };
+  // Only the two waves without MFMA work (14: the 28 X chunks, 15: the 16 D
+  // chunks) stage: the scalar unit is shared by the CU's waves, and the
+  // per-chunk address / M0 work on all 16 waves cost ~0.8 us per band.  A row
+  // outside the image is zeroed by ds_write and its DMA goes to the scratch
+  // KiB, so that each stager has a fixed count in flight (its vmcnt).
+  constexpr int NXD = 2 * XR, NDD = 2 * RB;
+  const unsigned scr = lds0 + WG16_DMA_BUFS * BE * 2;
+  auto issue = [&](int u) {
+    if (u >= nunits || wave < 14 || (PT_ABL(ablate) & 128)) return;
+    const unsigned xt = lds0 + (unsigned)((u % WG16_DMA_BUFS) * BE * 2);
+    const int f = g + (u / NB) * nwg, y0 = (u % NB) * RB;   // frame-clip f = t * B + b
+    if (wave == 14) {
+      const bf16_t* xb = Xs + (size_t)f * NPIX * C;
+#pragma unroll
+      for (int row = 0; row < XR; ++row) {
+        const int iy = y0 + row - PAD;
+        const bool in = iy >= 0 && iy < IMG;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const unsigned d = xt + wx_off<PAD>(row, PAD + half * 16, 0) * 2;
+          if (in) {
+            dma(xb + (iy * IMG + half * 16) * C, d);
+          } else {
+            *(__attribute__((address_space(3))) u32x4*)(size_t)(d + voff) = u32x4{0u, 0u, 0u, 0u};
+            dma(Ds, scr);
+          }
+        }
+      }
+    } else {
+      const bf16_t* db = Ds + (size_t)f * NPIX * C + (size_t)y0 * IMG * C;
+#pragma unroll
+      for (int k = 0; k < NDD; ++k) dma(db + k * 16 * C, xt + (XE + k * 16 * C) * 2);
+    }
+  };
+  // retire band v's DMAs: this stager's count for a band still in flight behind it
+  auto retire = [&](bool more) {
+    if (more && wave == 14) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NXD) : "memory");
+    else if (more && wave == 15) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NDD) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  issue(0);
+  issue(1);
+  retire(1 < nunits);                     // band 0 landed
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int u = 0; u < nunits; ++u) {
+    issue(u + 2);
+    int bo = (u % WG16_DMA_BUFS) * BE;
+    asm volatile("" : "+s"(bo));          // opaque: no per-buffer address sets hoisted out of the loop
+    bf16_t* xt = buf + bo;
+    if (!(PT_ABL(ablate) & 64)) body(xt, xt + XE);
+    retire(u + 2 < nunits);               // band u + 1 landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool DMA>
+__global__ __launch_bounds__(WG16_NT, 1) void k_wgrad16(CellArgs<bf16_t> a, float* wslab, int nwg, int conv0) {
+  constexpr int PAD = PADMAX;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* buf = (bf16_t*)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = blockIdx.x, conv = blockIdx.y + conv0;
+  const bf16_t* Xs = conv == 0 ? a.gE : a.Ic;
+  const bf16_t* Ds = conv == 0 ? a.dci_s : a.dce_s;
+  float* dst = wslab + ((size_t)conv * nwg + g) * 49 * 1024;
+  const int kw = (int)((WG16_KW >> (4 * wave)) & 15);
+  // one full copy of the band loop per unit shape (a shape branch inside the
+  // loop spilled 180 VGPRs)
+  auto unit = [&](auto kh0c, auto nkhc) {
+    constexpr int KH0 = decltype(kh0c)::value, NKH = decltype(nkhc)::value;
+    f32x16 acc[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = zero16();
+    auto body = [&](const bf16_t* xt, const bf16_t* dt) {
+      if (kw >= 7) return;
+      wgrad_band16<KH0, NKH>(acc, xt, dt, kw, lane);
+    };
+    if constexpr (DMA) wgrad_run_dma(body, Xs, Ds, a.B, a.T, g, nwg, buf, tid, wave, lane, a.ablate);
+    else wgrad_run<bf16_t, PAD, WG16_NT>(body, Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
+    if (kw >= 7) return;
+#pragma unroll
+    for (int j = 0; j < NKH; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[((KH0 + j) * 7 + kw) * 1024 + r * 64 + lane] = acc[j][r];
+    }
+  };
+  if ((WG16_BIG >> wave) & 1) unit(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+  else unit(std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{});
 }
 
 // =========================================================================
@@ -3188,7 +3366,7 @@ struct ReduceArgs {
   int part;             // 0: the per-clip slabs (all but the k x k weights); 1: the k x k weights
   int Cu;               // the caller's channel count (<= 32); padded channels are dropped
   const float* slab;    // [rows][SLAB]
-  const float* wslab;   // [2][nwg][K*K][1024]
+  const float* wslab;   // [2][nwg][K*K][16 r][64 lanes] (accumulator tiles, lane-linear)
   pt_cell_grads g;
 };
 
@@ -3268,7 +3446,9 @@ __global__ void k_reduce(ReduceArgs r) {
     } else {
       const int e2 = e - n_small;
       const int conv = e2 / (KK * 1024), rem = e2 % (KK * 1024);
-      const int tap = rem / 1024, nc = rem % 1024, n = nc / 32, ci = nc % 32;
+      // wslab tiles are stored lane-linear (k_wgrad: [r][lane] of the 32x32
+      // accumulator, 256-B stores): n = lane & 31, ci = cl_x(r, lane >> 5)
+      const int tap = rem / 1024, nc = rem % 1024, n = nc & 31, ci = cl_x(nc >> 6, (nc >> 5) & 1);
       const float s = strided_sum(r.wslab + ((size_t)conv * r.nwg * KK + tap) * 1024 + nc,
                                   (size_t)KK * 1024, r.nwg);
       float* W = conv == 0 ? r.g.w_inh : r.g.w_exc;
@@ -3697,6 +3877,10 @@ int set_lds_attrs() {
   SETLDS((k_persist_fwd<S, 1, 1>), fused_lds_bytes<S>());
   SETLDS((k_wgrad<S, PADMAX>), (wgrad_lds_bytes<S, PADMAX>()));
   SETLDS((k_wgrad<S, PADBIG>), (wgrad_lds_bytes<S, PADBIG>()));
+  if constexpr (sizeof(S) == 2) {
+    SETLDS(k_wgrad16<false>, (wgrad_lds_bytes<S, PADMAX>()));
+    SETLDS(k_wgrad16<true>, wgrad16_dma_lds_bytes());
+  }
   done = true;
   return 0;
 }
@@ -3777,6 +3961,17 @@ bool pwb2_env() {
 bool pwa2_env() {
   const char* e = getenv("PT_PWA2");
   return e && e[0] == '1';
+}
+// k_wgrad16 (bf16, k = 7) by default; PT_WG16=0 (read per call) selects the
+// 8-wave k_wgrad.
+bool wg16_env() {
+  const char* e = getenv("PT_WG16");
+  return !(e && e[0] == '0');
+}
+// its LDS-DMA band staging on untiled frames (PT_WGDMA=0: register staging)
+bool wgdma_env() {
+  const char* e = getenv("PT_WGDMA");
+  return !(e && e[0] == '0');
 }
 bool use_fused(const pt_cell_desc* d, const Plan& p) {
   return fused_env() && d->dtype == PT_DTYPE_BF16 && p.ntx * p.nty == 1 &&
@@ -3948,6 +4143,16 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
     if (d->no_inh) HIPCHK(zero_async(wslab, (size_t)p.nwg * p.K * p.K * 1024 * 4, st));
     timed(PT_K_WGRAD, st, [&] {
       const dim3 grid(p.nwg, 2 - conv0, wgrad_groups(p.K, sizeof(S) == 2));
+      if constexpr (sizeof(S) == 2)
+        if (p.K == 7 && wg16_env()) {
+          if (p.ntx * p.nty == 1 && wgdma_env())
+            hipLaunchKernelGGL(k_wgrad16<true>, grid, dim3(WG16_NT), wgrad16_dma_lds_bytes(), st, a, wslab, p.nwg,
+                               conv0);
+          else
+            hipLaunchKernelGGL(k_wgrad16<false>, grid, dim3(WG16_NT), (wgrad_lds_bytes<S, PADMAX>()), st, a, wslab,
+                               p.nwg, conv0);
+          return;
+        }
       if (p.K <= 2 * PADMAX + 1)
         hipLaunchKernelGGL((k_wgrad<S, PADMAX>), grid, dim3(wgrad_nt<S, PADMAX>()), (wgrad_lds_bytes<S, PADMAX>()), st, a,
                            wslab, p.nwg, conv0);
@@ -3984,7 +4189,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   // diagnostics only (env PT_CELL_DEBUG_STOP = n): return after the sweep's
   // first n launches, leaving the transients as that launch wrote them
   const bool pwb2 = pwb2_env(), pwa2 = pwa2_env();
-  const int nprod_b = p.B * (pwb2 ? pb2_wgpc<S>() : PWB_WGPC);     // BN0 backward producers
+  const int nprod_b = p.B * (pwb2 ? (a.hgru ? pb2_wgpc<S, 1>() : pb2_wgpc<S, 0>()) : PWB_WGPC);   // BN0 bwd producers
   const int nprod_a = p.B * (pwa2 ? pa2_wgpc<S>() : PWA_WGPC);     // BN1 backward producers
   auto launch_pwa = [&] {
     if (pwa2)
@@ -4012,7 +4217,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
     if (stop()) return 0;
     a.t = t;
     if (pwb2)
-      timed(PT_K_PW_BB, st, [&] { PW_LAUNCH_NT(k_pw_bb2, dim3(p.B * pb2_wgpc<S>()), (pb2_lds_bytes<S>()), PB2_NT); });
+      timed(PT_K_PW_BB, st, [&] { PW_LAUNCH_NT(k_pw_bb2, dim3(nprod_b), (pb2_lds_bytes<S>()), PB2_NT); });
     else
       timed(PT_K_PW_BB, st, [&] { PW_LAUNCH(k_pw_bb, gpb, lpb); });
     if (stop()) return 0;
@@ -4142,7 +4347,7 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
       if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
       ptg::Key k;
       k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
-          .add(band_env()).add(pwb2_env()).add(pwa2_env()).add(xmap_env());
+          .add(band_env()).add(pwb2_env()).add(pwa2_env()).add(xmap_env()).add(wg16_env()).add(wgdma_env());
       rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
     }
     if (rc) return rc;

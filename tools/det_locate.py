@@ -170,7 +170,7 @@ def main():
         bp1 = w1[L["bnb_part"]:L["bnb_part"] + t * 2 * b * WGPC * 256].view(torch.float32).view(t, 2, b * WGPC, 64)
         for tt in range(t - 1, -1, -1):
             for bn in (0, 1):
-                pb2 = os.environ.get("PT_PWB2", "1") != "0"     # k_pw_bb2: 2 (bf16) / 8 (f32) producers per clip
+                pb2 = os.environ.get("PT_PWB2", "1") != "0"     # k_pw_bb2: 2 (bf16) / 8 (f32) producers per clip (InT; hGRU bf16 uses 4)
                 nprod = b * (((2 if es == 2 else 8) if pb2 else WGPC) if bn == 0 else 2)
                 pd = (bp0[tt, bn, :nprod] != bp1[tt, bn, :nprod]).any(1).nonzero().flatten().tolist()
                 gd = (bg0[tt, bn] != bg1[tt, bn]).any(1).nonzero().flatten().tolist()
