@@ -3172,10 +3172,11 @@ constexpr int WG16_DMA_BUFS = 3;
 constexpr int wgrad16_dma_lds_bytes() {
   return WG16_DMA_BUFS * wgrad_band_elems<bf16_t, PADMAX>() * 2 + 1024;
 }
-template <class Body>
+template <bool TILED, class Body>
 __device__ __forceinline__ void wgrad_run_dma(Body&& body, const bf16_t* __restrict__ Xs,
                                               const bf16_t* __restrict__ Ds, int B, int T, int g, int nwg,
-                                              bf16_t* buf, int tid, int wave, int lane, int ablate) {
+                                              bf16_t* buf, int tid, int wave, int lane, int ablate, int ntx,
+                                              int nty) {
   constexpr int PAD = PADMAX;
   constexpr int BE = wgrad_band_elems<bf16_t, PAD>();
   constexpr int RB = wg_rb<bf16_t, PAD>(), XR = wg_xr<bf16_t, PAD>(), NB = IMG / RB;
@@ -3200,33 +3201,60 @@ __device__ __forceinline__ void wgrad_run_dma(Body&& body, const bf16_t* __restr
   // per-chunk address / M0 work on all 16 waves cost ~0.8 us per band.  A row
   // outside the image is zeroed by ds_write and its DMA goes to the scratch
   // KiB, so that each stager has a fixed count in flight (its vmcnt).
-  constexpr int NXD = 2 * XR, NDD = 2 * RB;
+  // tiled frames (TILED): the X halo rows come from the tiles above / below,
+  // and each row's 3 + 3 halo pixels (192 B each side) from the left / right
+  // neighbours as 12-lane DMAs -- wave 14 the left, wave 15 the right ones
+  constexpr int NXD = 2 * XR + (TILED ? XR : 0), NDD = 2 * RB + (TILED ? XR : 0);
   const unsigned scr = lds0 + WG16_DMA_BUFS * BE * 2;
   auto issue = [&](int u) {
     if (u >= nunits || wave < 14 || (PT_ABL(ablate) & 128)) return;
     const unsigned xt = lds0 + (unsigned)((u % WG16_DMA_BUFS) * BE * 2);
     const int f = g + (u / NB) * nwg, y0 = (u % NB) * RB;   // frame-clip f = t * B + b
+    int ty = 0, tx = 0;
+    if constexpr (TILED) {
+      const TileLoc L = tile_loc(f % B, ntx, nty);
+      ty = L.ty; tx = L.tx;
+    }
+    // halo pixels of X row `row` on side sd (0 left, 1 right): 12 lanes x 16 B
+    auto halo = [&](int row, int sd) {
+      const int iy = y0 + row - PAD, dy = iy < 0 ? -1 : (iy >= IMG ? 1 : 0), dx = sd ? 1 : -1;
+      const bool ok = ty + dy >= 0 && ty + dy < nty && tx + dx >= 0 && tx + dx < ntx;
+      const unsigned d = xt + wx_off<PAD>(row, sd ? IMG + PAD : 0, 0) * 2;
+      if (lane < 3 * C * 2 / 16) {
+        if (ok) {
+          dma(Xs + ((size_t)f + dy * ntx + dx) * NPIX * C + ((iy - dy * IMG) * IMG + (sd ? 0 : IMG - PAD)) * C, d);
+        } else {
+          *(__attribute__((address_space(3))) u32x4*)(size_t)(d + voff) = u32x4{0u, 0u, 0u, 0u};
+          dma(Ds, scr);
+        }
+      }
+    };
     if (wave == 14) {
-      const bf16_t* xb = Xs + (size_t)f * NPIX * C;
 #pragma unroll
       for (int row = 0; row < XR; ++row) {
-        const int iy = y0 + row - PAD;
-        const bool in = iy >= 0 && iy < IMG;
+        const int iy = y0 + row - PAD, dy = iy < 0 ? -1 : (iy >= IMG ? 1 : 0);
+        const bool in = TILED ? (ty + dy >= 0 && ty + dy < nty) : dy == 0;
+        const bf16_t* xb = Xs + ((size_t)f + dy * ntx) * NPIX * C + (size_t)(iy - dy * IMG) * IMG * C;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const unsigned d = xt + wx_off<PAD>(row, PAD + half * 16, 0) * 2;
           if (in) {
-            dma(xb + (iy * IMG + half * 16) * C, d);
+            dma(xb + half * 16 * C, d);
           } else {
             *(__attribute__((address_space(3))) u32x4*)(size_t)(d + voff) = u32x4{0u, 0u, 0u, 0u};
             dma(Ds, scr);
           }
         }
+        if constexpr (TILED) halo(row, 0);
       }
     } else {
       const bf16_t* db = Ds + (size_t)f * NPIX * C + (size_t)y0 * IMG * C;
 #pragma unroll
-      for (int k = 0; k < NDD; ++k) dma(db + k * 16 * C, xt + (XE + k * 16 * C) * 2);
+      for (int k = 0; k < 2 * RB; ++k) dma(db + k * 16 * C, xt + (XE + k * 16 * C) * 2);
+      if constexpr (TILED) {
+#pragma unroll
+        for (int row = 0; row < XR; ++row) halo(row, 1);
+      }
     }
   };
   // retire band v's DMAs: this stager's count for a band still in flight behind it
@@ -3277,7 +3305,12 @@ __global__ __launch_bounds__(WG16_NT, 1) void k_wgrad16(CellArgs<bf16_t> a, floa
       if (kw >= 7) return;
       wgrad_band16<KH0, NKH>(acc, xt, dt, kw, lane);
     };
-    if constexpr (DMA) wgrad_run_dma(body, Xs, Ds, a.B, a.T, g, nwg, buf, tid, wave, lane, a.ablate);
+    if constexpr (DMA) {
+      if (a.ntx * a.nty > 1)
+        wgrad_run_dma<true>(body, Xs, Ds, a.B, a.T, g, nwg, buf, tid, wave, lane, a.ablate, a.ntx, a.nty);
+      else
+        wgrad_run_dma<false>(body, Xs, Ds, a.B, a.T, g, nwg, buf, tid, wave, lane, a.ablate, 1, 1);
+    }
     else wgrad_run<bf16_t, PAD, WG16_NT>(body, Xs, Ds, a.B, a.T, g, nwg, buf, tid, a.ablate, a.ntx, a.nty);
     if (kw >= 7) return;
 #pragma unroll
@@ -4145,7 +4178,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       const dim3 grid(p.nwg, 2 - conv0, wgrad_groups(p.K, sizeof(S) == 2));
       if constexpr (sizeof(S) == 2)
         if (p.K == 7 && wg16_env()) {
-          if (p.ntx * p.nty == 1 && wgdma_env())
+          if (wgdma_env())
             hipLaunchKernelGGL(k_wgrad16<true>, grid, dim3(WG16_NT), wgrad16_dma_lds_bytes(), st, a, wslab, p.nwg,
                                conv0);
           else

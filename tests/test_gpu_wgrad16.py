@@ -6,8 +6,8 @@ bands and accumulate in f32; only the order of the per-tile MFMA sums differs
 the two k x k weight gradients agree to 1e-5 relative and every other gradient
 is bitwise equal.  Also: two runs of the default are bitwise equal, the
 LDS-DMA band staging (default on untiled frames) equals the register staging
-(PT_WGDMA=0) bitwise, and a 64x64 (tiled, halo-staged) hGRU frame goes
-through the register-staged 16-wave kernel."""
+(PT_WGDMA=0) bitwise, also on 64x64 (tiled) hGRU frames, whose X halo rows
+and columns come from the neighbouring tiles."""
 import os
 
 import numpy as np
