@@ -76,6 +76,7 @@ struct LConvArgs {
   const float* add;     // f32, same layout as out, or null
   const float* bias;    // f32 [32*NO] or null
   int nimg;
+  int fast;             // bf16, k <= 7: the prefetching column loop (PT_LCONV_FAST=0: the plain one)
 };
 
 // out[img][p][32 o + n] = sum_{ig, ci, tap} W[o, ig][n][ci][tap] src[img][p + tap][32 ig + ci]
@@ -115,6 +116,93 @@ __global__ __launch_bounds__(NT, conv_occ<NO>()) void k_lconv(LConvArgs a) {
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i] = zero16();
 
+  // bf16, k <= 7 (r04): the next kernel column's weight fragments are loaded
+  // under the current column's MFMAs (ping-pong registers; loading them at the
+  // column start exposed an L2 round trip per column), and the transposed
+  // conv's next input group is loaded into registers under the current group's
+  // columns and stored to the tile between two barriers afterwards.  Same MFMA
+  // order per accumulator as the loop below (bitwise equal).
+  constexpr bool FAST = sizeof(S) == 2 && K <= 7;
+  bool done = false;
+  if constexpr (FAST) if (a.fast) {
+    done = true;
+    u32x4 v[PER];
+    auto ld_tile = [&](int ig) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx0 = tid + k * NT;
+        const int idx = idx0 < NCHUNK ? idx0 : NCHUNK - 1;
+        const int q = idx % NCH, pc = idx / NCH, col = pc % IMG, row = pc / IMG;
+        const int iy = y0 + row - L::P;
+        const int cy = iy < 0 ? 0 : (iy >= IMG ? IMG - 1 : iy);
+        v[k] = *(const u32x4*)(src + (size_t)(cy * IMG + col) * SRCC + ig * 32 + q * CPB);
+        if (iy != cy) v[k] = u32x4{0u, 0u, 0u, 0u};
+      }
+    };
+    auto st_tile = [&]() {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = tid + k * NT;
+        if (PER * NT == NCHUNK || idx < NCHUNK) {
+          const int q = idx % NCH, pc = idx / NCH, col = pc % IMG, row = pc / IMG;
+          *(u32x4*)(tile + L::off(row, col + L::P, q * CPB)) = v[k];
+        }
+      }
+    };
+    ld_tile(0);
+    __syncthreads();                       // the clear is done
+    st_tile();
+    __syncthreads();
+    constexpr int NC = NI * K;             // (input group, kernel column) steps
+    F wa[K][KSP], wb[K][KSP];
+    auto ld_w = [&](int c, F (&w)[K][KSP]) {
+      const int ig = c / K, kw = c - ig * K;
+      const F* wk = wf + ((size_t)((o * NI + ig) * KK + kw) * TT::KS) * 64 + lane;
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+        for (int s2 = 0; s2 < KSP; ++s2) w[kh][s2] = wk[((size_t)kh * K * TT::KS + s2) * 64];
+    };
+    auto step = [&](int c, const F (&bc)[K][KSP], F (&nx)[K][KSP]) {
+      const int ig = c / K, kw = c - ig * K;
+      if (c + 1 < NC) ld_w(c + 1, nx);
+      if (NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1);
+      __builtin_amdgcn_sched_barrier(0);   // the loads go out before this column's MFMAs
+      const int tcol = px + kw;
+      F av[NTR][KSP];
+      auto load_a = [&](int tr) {
+        const int trow = r0 + tr;
+#pragma unroll
+        for (int s2 = 0; s2 < KSP; ++s2) av[tr][s2] = *(const bf16x8*)(tile + L::off(trow, tcol, 16 * s2 + 8 * h));
+      };
+      constexpr int PF = 3 < NTR ? 3 : NTR;
+#pragma unroll
+      for (int tr = 0; tr < PF; ++tr) load_a(tr);
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr) {
+        if (tr + PF < NTR) load_a(tr + PF);
+#pragma unroll
+        for (int s2 = 0; s2 < KSP; ++s2) {
+#pragma unroll
+          for (int kh = 0; kh < K; ++kh) {
+            const int i = tr - kh;
+            if (i >= 0 && i < RW) acc[i] = TT::mma(bc[kh][s2], av[tr][s2], acc[i]);
+          }
+        }
+      }
+      if (NI > 1 && kw == K - 1 && ig + 1 < NI) {
+        __syncthreads();                   // every wave is done with this group's tile
+        st_tile();
+        __syncthreads();
+      }
+    };
+    ld_w(0, wa);
+    for (int c = 0; c < NC; c += 2) {
+      step(c, wa, wb);
+      if (c + 1 < NC) step(c + 1, wb, wa);
+    }
+  }
+  if (!done)
   for (int ig = 0; ig < NI; ++ig) {
     for (int pass = 0; pass < TT::NPASS; ++pass) {
       // ---- fill the band tile (rows outside the image are written as zeros;
@@ -970,11 +1058,16 @@ LPlan plan(const pt_lstm_desc* d) {
     default: { constexpr int KC = 15; CALL; } break;       \
   }
 
+// PT_LCONV_FAST=0 (read per call) selects k_lconv's plain column loop (A/B test)
+int lconv_fast_env() {
+  const char* e = getenv("PT_LCONV_FAST");
+  return !(e && e[0] == '0');
+}
 template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
          hipStream_t st) {
   using L = LTile<S, K, conv_rb<NO>()>;
-  LConvArgs a{src, wf, out, add, bias, nimg};
+  LConvArgs a{src, wf, out, add, bias, nimg, lconv_fast_env()};
   hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(NT),
                      L::BYTES, st, a);
   HIPCHK(hipGetLastError());
@@ -1237,7 +1330,7 @@ int pt_lstm_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params*
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out);
+  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out).add(lconv_fast_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
@@ -1255,7 +1348,7 @@ int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace, 
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g);
+  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 

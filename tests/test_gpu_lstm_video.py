@@ -81,6 +81,39 @@ def test_video_convlstm_bf16_tolerance():
             assert cos > 0.99, (n, cos)
 
 
+def test_lconv_prefetch_loop_is_bitwise_the_plain_loop():
+    """k_lconv's prefetching column loop (bf16, k <= 7, r04) against its plain
+    loop (PT_LCONV_FAST=0): the same MFMA order per accumulator, so logits, the
+    Jacobian penalty and every gradient are bitwise equal (k=7 and k=3)."""
+    import os
+    dev = _dev()
+    for k in (7, 3):
+        m = _model(k, 11 + k).to(dev).train()
+        m.cell_dtype = "bf16"
+        x, y = _clips(13 + k, 6, 5)
+        x, y = x.to(dev), y.to(dev).reshape(-1, 1)
+        res = []
+        old = os.environ.get("PT_LCONV_FAST")
+        try:
+            for v in ("0", "1"):
+                os.environ["PT_LCONV_FAST"] = v
+                m.zero_grad(set_to_none=True)
+                out, jv = m(x)
+                F.binary_cross_entropy_with_logits(out, y).backward()
+                torch.cuda.synchronize()
+                res.append((out.detach().clone(), jv.detach().clone(),
+                            {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+        finally:
+            if old is None:
+                os.environ.pop("PT_LCONV_FAST", None)
+            else:
+                os.environ["PT_LCONV_FAST"] = old
+        (o0, j0, g0), (o1, j1, g1) = res
+        assert torch.equal(o0, o1) and torch.equal(j0, j1), k
+        for n in g0:
+            assert torch.equal(g0[n], g1[n]), (k, n)
+
+
 def test_registry_builds_it():
     import types
     from utils import engine
