@@ -600,6 +600,153 @@ __global__ __launch_bounds__(NT, 1) void k_lwgrad(LWgradArgs a) {
   }
 }
 
+// bf16, k <= 7 (r04): the same sums with workgroup (kw, slice) owning kernel
+// COLUMN kw (wave g: gate g, accumulator tiles kh = 0 .. K-1).  k_lwgrad reads
+// one shifted X fragment per tap and MFMA (7 X + 1 D transposed reads per 7
+// MFMAs: bound by the LDS reads); here the band's D fragments stay in
+// registers and each X-row fragment (shift kw) feeds the MFMAs of all K kernel
+// rows, as InT's k_wgrad does: (RB + K - 1) * 2 X reads + RB * 2 D reads per
+// RB * 2 * K MFMAs.  The X band carries the K - 1 halo rows.  Same MFMA order
+// per tile as k_lwgrad (D row, then pixel block): bitwise equal.
+template <int K> struct LWBand2 {
+  using S = bf16_t;
+  static constexpr int P = K / 2;
+  static constexpr int TC = IMG + K - 1;
+  static constexpr int RBW = lw_rb<S>();
+  static constexpr int XR = RBW + K - 1;                // X rows (with the vertical halo)
+  static constexpr int CPB = 8;
+  static constexpr int XE = XR * TC * HC;
+  static constexpr int DE = RBW * IMG * GC;
+  static constexpr int BE = XE + DE;
+  static constexpr int XPER = XR * IMG * (HC / CPB) / NT;
+  static constexpr int DPER = RBW * IMG * (GC / CPB) / NT;
+  static constexpr int BYTES = 2 * BE * 2;
+  static_assert(XR * IMG * (HC / CPB) % NT == 0, "X band split");
+  u32x4 x[XPER], d[DPER];
+  int xvalid;
+  __device__ __forceinline__ void load(const S* __restrict__ X, const S* __restrict__ D, int y0, int tid) {
+    xvalid = 0;
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % (HC / CPB), pc = idx / (HC / CPB), col = pc % IMG, row = pc / IMG;
+      const int iy = y0 + row - P;
+      const bool ok = iy >= 0 && iy < IMG;
+      x[j] = *(const u32x4*)(X + (size_t)((ok ? iy : 0) * IMG + col) * HC + q * CPB);
+      xvalid |= (int)ok << j;
+    }
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % (GC / CPB), pc = idx / (GC / CPB);
+      d[j] = *(const u32x4*)(D + (size_t)(y0 * IMG + pc) * GC + q * CPB);
+    }
+  }
+  __device__ __forceinline__ void store(S* xt, S* dt, int tid) const {
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int idx = tid + j * NT;
+      const int q = idx % (HC / CPB), pc = idx / (HC / CPB), col = pc % IMG, row = pc / IMG;
+      *(u32x4*)(xt + (row * TC + col + P) * HC + q * CPB) = (xvalid >> j) & 1 ? x[j] : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) *(u32x4*)(dt + (tid + j * NT) * CPB) = d[j];
+  }
+};
+
+template <int K>
+__global__ __launch_bounds__(NT, 1) void k_lwgrad2(LWgradArgs a) {
+  using S = bf16_t;
+  using Bd = LWBand2<K>;
+  constexpr int KK = K * K, RBW = Bd::RBW, NBW = IMG / RBW, TC = Bd::TC, XR = Bd::XR;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  S* buf = (S*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);     // gate of this wave
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;         // XCD-aware, as k_lwgrad
+  const int kw = j % K, sl = xcd + 8 * (j / K);
+  if (sl >= a.nsl) return;
+  const int nimg = a.n0 + a.n1;
+  const int nmine = nimg > sl ? (nimg - sl + a.nsl - 1) / a.nsl : 0;
+  const int nunits = nmine * NBW;
+
+  f32x16 acc[K];
+#pragma unroll
+  for (int m = 0; m < K; ++m) acc[m] = zero16();
+  for (int i = tid; i < Bd::BYTES / 16; i += NT) ((u32x4*)buf)[i] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  auto unit_src = [&](int u, const S*& X, const S*& D, int& y0) {
+    const int jj = sl + (u / NBW) * a.nsl;
+    y0 = (u % NBW) * RBW;
+    if (jj < a.n0) {
+      X = (const S*)a.X0 + (size_t)jj * NPIX * HC;
+      D = (const S*)a.D0 + (size_t)jj * NPIX * GC;
+    } else {
+      X = (const S*)a.X1 + (size_t)(jj - a.n0) * NPIX * HC;
+      D = (const S*)a.D1 + (size_t)(jj - a.n0) * NPIX * GC;
+    }
+  };
+  Bd band;
+  if (nunits > 0) {
+    const S *X, *D;
+    int y0;
+    unit_src(0, X, D, y0);
+    band.load(X, D, y0, tid);
+    band.store(buf, buf + Bd::XE, tid);
+  }
+  __syncthreads();
+  const int grp = lane >> 4, m16 = lane & 15, q = m16 >> 2, pp = m16 & 3;
+  const int chb = 16 * (grp & 1) + 4 * pp, hh = grp >> 1;
+  for (int u = 0; u < nunits; ++u) {
+    int bo = (u & 1) * Bd::BE;
+    asm volatile("" : "+s"(bo));              // opaque: no per-buffer address sets hoisted
+    const S* xt = buf + bo;
+    const S* dt = xt + Bd::XE;
+    const bool more = u + 1 < nunits;
+    if (more) {
+      const S *X, *D;
+      int y0;
+      unit_src(u + 1, X, D, y0);
+      band.load(X, D, y0, tid);
+    }
+    // steps (X row r, pixel block blk), r outer: per tile (kh) the D rows
+    // yd = r - kh then the blocks, k_lwgrad's order
+    bf16x8 dv[RBW][2], av[2];
+    auto xaddr = [&](int st) {
+      return xt + ((st >> 1) * TC + (st & 1) * 16 + 8 * hh + q + kw) * HC + chb;
+    };
+#pragma unroll
+    for (int yd = 0; yd < RBW; ++yd)
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+        dv[yd][blk] = tr_read8<GC>(dt + (yd * IMG + blk * 16 + 8 * hh + q) * GC + g * 32 + chb);
+    av[0] = tr_read8<HC>(xaddr(0));
+#pragma unroll
+    for (int st = 0; st < 2 * XR; ++st) {
+      const int r = st >> 1, blk = st & 1, cur = st & 1;
+      if (st + 1 < 2 * XR) av[cur ^ 1] = tr_read8<HC>(xaddr(st + 1));
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        const int yd = r - kh;
+        if (yd >= 0 && yd < RBW) acc[kh] = Tr<S>::mma(av[cur], dv[yd][blk], acc[kh]);
+      }
+    }
+    if (more) {
+      S* xn = buf + ((u + 1) & 1) * Bd::BE;
+      band.store(xn, xn + Bd::XE, tid);
+      __syncthreads();
+    }
+  }
+  // acc[kh]: rows ci = cl_x(r, h), cols co = lane & 31 (k_lwgrad's slab layout)
+  float* dst = a.wslab + ((size_t)sl * NG + g) * KK * 1024;
+  const int co = lane & 31;
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[(kh * K + kw) * 1024 + co * 32 + cl_x(r, h)] = acc[kh][r];
+  }
+}
+
 // ------------------------------------------------------------- reductions
 // Column sums of [npix][GC] rows (the bias gradients): dPsum (static x) or, per-step
 // input, the rows of every step's dP_t (npix = T * B * NPIX), read in S.
@@ -1082,9 +1229,24 @@ int conv_k(int K, const void* src, const void* wf, float* out, const float* add,
   return rc;
 }
 
+// k_lwgrad2 for bf16 k <= 7: opt-in (PT_LWGRAD2=1, read per call).  Measured
+// r04 (cfg3, profiles/r04_lwgrad2_ab.txt): 47.56 vs 46.96 ms per step for
+// k_lwgrad -- its 2.3x fewer LDS reads did not pay for the 2.5x taller X band
+// (the K - 1 halo rows) and the D fragments read at every band start.
+int lwgrad2_env() {
+  const char* e = getenv("PT_LWGRAD2");
+  return e && e[0] == '1';
+}
 template <class S, int K>
 int wgrad(const LWgradArgs& a, hipStream_t st) {
   using Bd = LWBand<S, K>;
+  if constexpr (sizeof(S) == 2 && K <= 7) {
+    if (lwgrad2_env()) {
+      hipLaunchKernelGGL((k_lwgrad2<K>), dim3(K * ((a.nsl + 7) / 8) * 8), dim3(NT), LWBand2<K>::BYTES, st, a);
+      HIPCHK(hipGetLastError());
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((k_lwgrad<S, K>), dim3(K * ((a.nsl + 7) / 8) * 8), dim3(NT), Bd::BYTES, st, a);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1106,6 +1268,7 @@ int prime_k() {
   SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<4>()>::BYTES));
   SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<1>()>::BYTES));
   SETLDS((k_lwgrad<S, K>), (LWBand<S, K>::BYTES));
+  if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lwgrad2<K>), (LWBand2<K>::BYTES));
   done = true;
   return 0;
 }
@@ -1330,7 +1493,7 @@ int pt_lstm_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params*
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out).add(lconv_fast_env());
+  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out).add(lconv_fast_env()).add(lwgrad2_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
@@ -1348,7 +1511,7 @@ int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace, 
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env());
+  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env()).add(lwgrad2_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 

@@ -81,22 +81,25 @@ def test_video_convlstm_bf16_tolerance():
             assert cos > 0.99, (n, cos)
 
 
-def test_lconv_prefetch_loop_is_bitwise_the_plain_loop():
-    """k_lconv's prefetching column loop (bf16, k <= 7, r04) against its plain
-    loop (PT_LCONV_FAST=0): the same MFMA order per accumulator, so logits, the
-    Jacobian penalty and every gradient are bitwise equal (k=7 and k=3)."""
+@pytest.mark.parametrize("switch", ["PT_LCONV_FAST", "PT_LWGRAD2"])
+def test_lconv_prefetch_loop_is_bitwise_the_plain_loop(switch):
+    """r04 bf16 k <= 7 kernels against the forms they replace, switched off per
+    call: k_lconv's prefetching column loop (PT_LCONV_FAST=0: the plain loop)
+    and the column-owned weight gradients k_lwgrad2 (PT_LWGRAD2=0: k_lwgrad).
+    Same MFMA order per accumulator, so logits, the Jacobian penalty and every
+    gradient are bitwise equal (k=7, 5 and 3)."""
     import os
     dev = _dev()
-    for k in (7, 3):
+    for k in (7, 5, 3):
         m = _model(k, 11 + k).to(dev).train()
         m.cell_dtype = "bf16"
         x, y = _clips(13 + k, 6, 5)
         x, y = x.to(dev), y.to(dev).reshape(-1, 1)
         res = []
-        old = os.environ.get("PT_LCONV_FAST")
+        old = os.environ.get(switch)
         try:
             for v in ("0", "1"):
-                os.environ["PT_LCONV_FAST"] = v
+                os.environ[switch] = v
                 m.zero_grad(set_to_none=True)
                 out, jv = m(x)
                 F.binary_cross_entropy_with_logits(out, y).backward()
@@ -105,9 +108,9 @@ def test_lconv_prefetch_loop_is_bitwise_the_plain_loop():
                             {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
         finally:
             if old is None:
-                os.environ.pop("PT_LCONV_FAST", None)
+                os.environ.pop(switch, None)
             else:
-                os.environ["PT_LCONV_FAST"] = old
+                os.environ[switch] = old
         (o0, j0, g0), (o1, j1, g1) = res
         assert torch.equal(o0, o1) and torch.equal(j0, j1), k
         for n in g0:
