@@ -46,10 +46,18 @@ constexpr int KMAX = 15;
 // column-start waits; 8 rows at one wave per SIMD ran 120 us per launch), the
 // whole image for the 4-gates-in transposed conv (one output tile: each wave
 // takes 8 rows, reusing every LDS fragment across 8 output rows)
-template <int NO> constexpr int conv_rb() { return NO == 4 ? 4 : IMG; }
+#ifndef PT_LCONV_RB
+#define PT_LCONV_RB 4       // (experiments: 8 rows per 4-gate workgroup, one wave per SIMD)
+#endif
+#ifndef PT_LCONVT_RB
+#define PT_LCONVT_RB 32     // (experiments: 16-row bands of the transposed conv, two per CU)
+#endif
+template <int NO> constexpr int conv_rb() { return NO == 4 ? PT_LCONV_RB : PT_LCONVT_RB; }
 // workgroups per CU the register budget allows (NO = 4: 4 rows per wave, two
 // waves per SIMD; NO = 1: 8 rows per wave over 4 input groups, one)
-template <int NO> constexpr int conv_occ() { return NO == 4 ? 2 : 1; }
+template <int NO> constexpr int conv_occ() {
+  return NO == 4 ? (PT_LCONV_RB == 4 ? 2 : 1) : (PT_LCONVT_RB == 16 ? 2 : 1);
+}
 
 // ------------------------------------------------------------------ conv tile
 template <class S, int K, int RB> struct LTile {
@@ -166,7 +174,9 @@ __global__ __launch_bounds__(NT, conv_occ<NO>()) void k_lconv(LConvArgs a) {
     auto step = [&](int c, const F (&bc)[K][KSP], F (&nx)[K][KSP]) {
       const int ig = c / K, kw = c - ig * K;
       if (c + 1 < NC) ld_w(c + 1, nx);
-      if (NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1);
+      // (two workgroups per CU: the registers are not there, the other one covers the fill)
+      constexpr bool TPF = conv_occ<NO>() == 1;
+      if (TPF && NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1);
       __builtin_amdgcn_sched_barrier(0);   // the loads go out before this column's MFMAs
       const int tcol = px + kw;
       F av[NTR][KSP];
@@ -191,6 +201,7 @@ __global__ __launch_bounds__(NT, conv_occ<NO>()) void k_lconv(LConvArgs a) {
         }
       }
       if (NI > 1 && kw == K - 1 && ig + 1 < NI) {
+        if (!TPF) ld_tile(ig + 1);
         __syncthreads();                   // every wave is done with this group's tile
         st_tile();
         __syncthreads();
