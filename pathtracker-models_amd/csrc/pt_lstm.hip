@@ -435,7 +435,10 @@ __global__ void k_ljv_final(const float* __restrict__ jdh, const float* __restri
 // (kh, slice): wave g owns gate g and the K taps of kernel row kh (K
 // accumulator tiles); D / X row bands are staged in LDS (double-buffered,
 // register prefetch), fragments come from ds_read_b64_tr_b16 transposed reads.
-template <class S> constexpr int lw_rb() { return sizeof(S) == 2 ? 4 : 2; }   // D rows per band
+#ifndef PT_LW_RB
+#define PT_LW_RB 2          // bf16 D rows per weight-gradient band (r04: 2, two workgroups per CU)
+#endif
+template <class S> constexpr int lw_rb() { return sizeof(S) == 2 ? PT_LW_RB : 2; }   // D rows per band
 template <class S, int K> struct LWBand {
   static constexpr int P = K / 2;
   static constexpr int TC = IMG + K - 1;
