@@ -82,3 +82,36 @@ def test_wgrad16_matches_wgrad8(kind):
         err = float((a - ref).abs().max())
         assert err <= 1e-5 * float(ref.abs().max()), (k, err)
     assert nk <= 2
+
+
+@pytest.mark.parametrize("kind,b,t", [("int", 1, 1), ("int", 3, 2), ("int", 2, 3), ("hgru64", 1, 1),
+                                      ("hgru64", 1, 2)])
+def test_wgrad16_smallest_shapes(kind, b, t):
+    """Fewer (frame, clip) pairs than workgroups (B*T = 1..6): one or two band
+    units per workgroup, so the LDS-DMA prologue and drain run with nothing or
+    one band behind them; equal to the 8-wave kernel as above."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from models import InT, ffhgru_hierarchy
+    from ptamd import synth
+    dev = torch.device("cuda:0")
+    torch.manual_seed(b * 10 + t)
+    hw = 64 if kind == "hgru64" else 32
+    if kind == "hgru64":
+        m = ffhgru_hierarchy.FFhGRU(dimensions=32, timesteps=t, kernel_size=7)
+    else:
+        m = InT.InT(dimensions=32, timesteps=t, kernel_size=7)
+    m = m.to(dev)
+    m.cell_dtype = "bf16"
+    clips, labels = synth.make_batch(50 + b + t, b, t, h=hw, w=hw)
+    x = torch.from_numpy(np.ascontiguousarray(clips.transpose(0, 4, 1, 2, 3), dtype=np.float32) / 255.0).to(dev)
+    y = torch.tensor([ord(v) for v in labels], dtype=torch.float32, device=dev)
+    g8 = _with_env("PT_WG16", "0", lambda: _grads(m, x, y))
+    g16 = _grads(m, x, y)
+    greg = _with_env("PT_WGDMA", "0", lambda: _grads(m, x, y))
+    for k in g8:
+        a, ref = g16[k], g8[k]
+        assert torch.isfinite(a).all(), k
+        assert torch.equal(a, greg[k]), ("DMA vs register staging", k)
+        err = float((a - ref).abs().max())
+        assert err <= 1e-5 * float(ref.abs().max()) + 1e-12, (k, err)
