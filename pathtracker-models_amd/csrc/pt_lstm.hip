@@ -94,8 +94,9 @@ struct LConvArgs {
 // with row reuse as in pt_device.h conv_run_k: each B fragment (tile row,
 // kw, k-step) is read from LDS once and feeds the K MFMAs of the output rows
 // it contributes to.  Wave w: output tile o = w % NO, rows (w / NO) * RW ...
-template <class S, int K, int NI, int NO>
-__global__ __launch_bounds__(NT, conv_occ<NO>()) void k_lconv(LConvArgs a) {
+template <class S, int K, int NI, int NO, int NTH = NT>
+__global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
+  constexpr int NT = NTH, NWAVE = NTH / 64;   // (8 waves: the transposed conv at two waves per SIMD)
   using TT = Tr<S>;
   using F = typename TT::frag;
   constexpr int RB = conv_rb<NO>(), NBAND = IMG / RB;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(NT, conv_occ<NO>()) void k_lconv(LConvArgs a) {
       const int ig = c / K, kw = c - ig * K;
       if (c + 1 < NC) ld_w(c + 1, nx);
       // (two workgroups per CU: the registers are not there, the other one covers the fill)
-      constexpr bool TPF = conv_occ<NO>() == 1;
+      constexpr bool TPF = conv_occ<NO>() == 1 && NTH == 256;
       if (TPF && NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1);
       __builtin_amdgcn_sched_barrier(0);   // the loads go out before this column's MFMAs
       const int tcol = px + kw;
@@ -1224,11 +1225,28 @@ int lconv_fast_env() {
   const char* e = getenv("PT_LCONV_FAST");
   return !(e && e[0] == '0');
 }
+// the transposed conv on 8 waves of 4 rows (two per SIMD) instead of 4 of 8:
+// opt-in (PT_LCONVT8=1, read per call).  Measured r04 (cfg3,
+// profiles/r04_lconvt8_ab.txt): 45.83 vs 45.64 ms per step -- the 256-VGPR
+// budget spills 42 registers and the 8 waves load the same weights twice as
+// often as 4.
+int lconvt8_env() {
+  const char* e = getenv("PT_LCONVT8");
+  return e && e[0] == '1';
+}
 template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
          hipStream_t st) {
   using L = LTile<S, K, conv_rb<NO>()>;
   LConvArgs a{src, wf, out, add, bias, nimg, lconv_fast_env()};
+  if constexpr (sizeof(S) == 2 && K <= 7 && NO == 1) {
+    if (lconvt8_env()) {
+      hipLaunchKernelGGL((k_lconv<S, K, NI, NO, 2 * NT>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(2 * NT),
+                         L::BYTES, st, a);
+      HIPCHK(hipGetLastError());
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(NT),
                      L::BYTES, st, a);
   HIPCHK(hipGetLastError());
@@ -1281,6 +1299,7 @@ int prime_k() {
   if (done) return 0;
   SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<4>()>::BYTES));
   SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<1>()>::BYTES));
+  if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lconv<S, K, 4, 1, 2 * NT>), (LTile<S, K, conv_rb<1>()>::BYTES));
   SETLDS((k_lwgrad<S, K>), (LWBand<S, K>::BYTES));
   if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lwgrad2<K>), (LWBand2<K>::BYTES));
   done = true;
@@ -1507,7 +1526,7 @@ int pt_lstm_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params*
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out).add(lconv_fast_env()).add(lwgrad2_env());
+  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
@@ -1525,7 +1544,7 @@ int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace, 
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env()).add(lwgrad2_env());
+  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
