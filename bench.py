@@ -21,9 +21,14 @@ weight-gradient kernel; --no-grad-overlap averages everything here).
 
 roofline: the dominant kernel (largest summed device time over K further,
 instrumented steps, measured with HIP events the library records around its
-own launches on the launch stream) against whichever roofline binds it — dense MFMA peak or
-HBM bandwidth — using the algorithmic FLOPs / bytes per launch of DESIGN.md §3;
-traffic = PMC-measured HBM bytes per launch from profiles/ (or null).
+own launches on the launch stream) against the roofline SURVEY.md §8(d) binds
+it to: MFMA for every kernel with a k x k conv (§8(d) FLOPs per launch / launch
+time / dense bf16 peak), HBM for the point-wise-only kernels (DESIGN.md §3
+bytes); mfma_frac and hbm_frac_design_bytes (the design's own byte count, a
+secondary figure) for every kernel; traffic = PMC-measured HBM bytes per launch
+from profiles/ (or null).  step_vs_8d: the whole step's §8(d) FLOPs against the
+MFMA peak (step_mfma_frac) and its PMC-measured bytes against §8(d)'s minimum
+(step_traffic_vs_8d).
 cpu_baseline: the CPU oracle
 (oracle/cells.py, plain PyTorch fp32, the reference's own op graph) timed on
 this host for a bounded sample (rank 0, N=1 only): B=4 clips of the workload's
@@ -123,6 +128,44 @@ def algorithmic_bytes(kind, batch, frames, elt, xb=4, fused=False):
         "k_wgrad": frames * 4 * F,
     }
     return per_clip.get(kind, 0) * batch
+
+
+# forward per clip-frame 2 k x k convs + 6 gates = 218,103,808 FLOP,
+# the stem 2*3*32*1024 per frame; fwd + bwd = 3 x forward (41.91 GFLOP / clip at
+# T = 64).  Minimal HBM bytes: 17.2 MB per 64-frame clip (268.75 KB per clip-frame).
+FLOP_8D_FRAME = 2 * conv_flops() + 6 * gate_flops()
+FLOP_8D_STEM = 2 * 3 * C * HW * HW
+BYTES_8D_FRAME = 17.2e6 / 64
+CONV_KINDS = ("k_fused_fa", "k_fused_fb", "k_conv_fa", "k_conv_fb", "k_conv_ba", "k_conv_bb", "k_wgrad",
+              "k_persist_fwd")
+
+
+def step_flops_8d(batch, frames):
+    return 3 * batch * frames * (FLOP_8D_FRAME + FLOP_8D_STEM)
+
+
+def _pmc_summary(batch, frames, dtype, lib_version):
+    import glob
+    tag = f"B={batch} T={frames} {dtype}"
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("note") == tag and d.get("lib_version") == lib_version:
+            return d
+    return None
+
+
+def pmc_step_bytes(batch, frames, dtype, lib_version):
+    """HBM bytes of one whole step from the matching PMC summary: every kernel's
+    per-launch traffic times its launches per profiled step (the summary's
+    `steps`, else the fused forward's launches / frames), or None."""
+    d = _pmc_summary(batch, frames, dtype, lib_version)
+    if d is None:
+        return None
+    k = d["kernels"]
+    steps = d.get("steps") or (k["k_fused_fa"]["launches"] / frames if "k_fused_fa" in k else None)
+    if not steps:
+        return None
+    return sum(v["traffic_bytes"] * v["launches"] for v in k.values()) / steps
 
 
 def pmc_traffic(kernel, batch, frames, dtype, lib_version):
@@ -228,20 +271,27 @@ def cpu_baseline(seconds, frames=64, batch=4):
 
 
 def kernel_roofline(kind, ms, n, batch, frames, steps, dtype, xb, fused=False):
-    """One kernel kind against whichever roofline binds it (the larger ideal
-    time: algorithmic FLOP / dense MFMA peak vs algorithmic bytes / HBM peak)."""
+    """One kernel kind against the roofline SURVEY.md §8(d) binds it to: every
+    kernel that runs a k x k conv (the fused cell segments, the backward convs,
+    the weight gradients) is MFMA-bound -- achieved = §8(d) FLOPs per launch /
+    average launch time vs the dense MFMA peak; the point-wise-only kernels
+    are HBM-bound on this design's algorithmic bytes.  Also
+    returned for every kernel: its MFMA fraction and, labelled as the
+    design's own byte count, its HBM fraction."""
     elt = 2 if dtype == "bf16" else 4
     fl = algorithmic_flops(kind, batch, frames, fused) * steps / max(n, 1)
     by = algorithmic_bytes(kind, batch, frames, elt, xb, fused) * steps / max(n, 1)
     avg = ms / max(n, 1) * 1e-3
     peak_f = PEAK_TFLOPS[dtype]
-    if fl / (peak_f * 1e12) >= by / (PEAK_HBM_GBS * 1e9):
-        r = {"bound": "mfma", "achieved": round(fl / avg / 1e12, 2), "peak": peak_f,
-             "unit": "TFLOP/s"}
+    mf = fl / avg / 1e12
+    hb = by / avg / 1e9
+    if kind in CONV_KINDS:
+        r = {"bound": "mfma", "achieved": round(mf, 2), "peak": peak_f, "unit": "TFLOP/s"}
     else:
-        r = {"bound": "hbm", "achieved": round(by / avg / 1e9, 1), "peak": PEAK_HBM_GBS,
-             "unit": "GB/s"}
+        r = {"bound": "hbm", "achieved": round(hb, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
     r["frac"] = round(r["achieved"] / r["peak"], 4)
+    r["mfma_frac"] = round(mf / peak_f, 4)
+    r["hbm_frac_design_bytes"] = round(hb / PEAK_HBM_GBS, 4)
     return r, int(fl), int(by), avg * 1e3
 
 
@@ -396,7 +446,19 @@ def main():
             r, _, _, a = kernel_roofline(k, ms, n, args.batch, args.frames, args.steps,
                                          args.dtype, xb, fused)
             per_kind[k] = {"bound": r["bound"], "achieved": r["achieved"], "unit": r["unit"],
-                           "frac": r["frac"], "avg_launch_us": round(a * 1e3, 2)}
+                           "frac": r["frac"], "mfma_frac": r["mfma_frac"],
+                           "hbm_frac_design_bytes": r["hbm_frac_design_bytes"],
+                           "avg_launch_us": round(a * 1e3, 2)}
+        # the whole step against SURVEY.md §8(d): its FLOPs vs the MFMA peak, and
+        # the PMC-measured HBM bytes of every kernel of the step vs §8(d)'s minimum
+        sf = step_flops_8d(world * args.batch, args.frames) / world
+        step_s = el / args.steps
+        sb = pmc_step_bytes(args.batch, args.frames, args.dtype, version)
+        step_8d = {"flop_per_step": int(sf), "step_mfma_frac": round(sf / step_s / (PEAK_TFLOPS[args.dtype] * 1e12), 4),
+                   "min_bytes_per_step_8d": int(args.batch * args.frames * BYTES_8D_FRAME),
+                   "pmc_bytes_per_step": None if sb is None else int(sb),
+                   "step_traffic_vs_8d": None if sb is None else
+                   round(sb / (args.batch * args.frames * BYTES_8D_FRAME), 2)}
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -419,6 +481,7 @@ def main():
                        "grad_overlap": world > 1 and not args.no_grad_overlap},
             "roofline": roof,
             "roofline_per_kernel": per_kind,
+            "step_vs_8d": step_8d,
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
             "allreduce_ms_per_step": round(ar_ms, 4),
             "lib_version": version,

@@ -2298,7 +2298,7 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
     const size_t ro = row_off(set);
     f32x2 sm[PB2_NQ];
 #pragma unroll
-    for (int q = 0; q < PB2_NQ; ++q) sm[q] = f32x2{0.f, 0.f};
+    for (int q = 0; q < PB2_NQ; ++q) sm[q] = f32x2{-0.f, -0.f};   // -0: the first add folds away
     const f32x4* xr = xs + set * PB2_NPX + px0 + 4 * g4;
     // this lane's channels 2n, 2n + 1
     float w0[2], w1[2], w2[2], bp[2];
@@ -2580,7 +2580,7 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_ba2(CellArgs<S> a) {
     if (!tail) GE = pr_load<float>(a.GEfin + ro, lane);
     f32x2 sm[PA2_NQ];
 #pragma unroll
-    for (int q = 0; q < PA2_NQ; ++q) sm[q] = f32x2{0.f, 0.f};
+    for (int q = 0; q < PA2_NQ; ++q) sm[q] = f32x2{-0.f, -0.f};
     if (tail) {
       const f32x4* xr = xs + set * PB2_NPX + px0 + 4 * g4;
       float w0[2], w1[2], w2[2], bp[2];
@@ -3688,11 +3688,8 @@ int debug_stop_env() {
 #endif
 }
 
-// PT_XCD_MAP=0 (read per call) selects the clip-major workgroup order (wg_split)
-int xmap_env() {
-  const char* e = getenv("PT_XCD_MAP");
-  return !(e && e[0] == '0');
-}
+// PT_XCD_MAP=0 (diagnostic builds only, read per call) selects the clip-major workgroup order (wg_split)
+int xmap_env() { return PT_SW("PT_XCD_MAP", 1); }
 
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
@@ -3926,16 +3923,13 @@ void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   else
     hipLaunchKernelGGL((k_conv_fwd<S, PADBIG>), dim3(p.B), dim3(NT), (conv_lds_bytes<S, PADBIG>()), st, c);
 }
-// PT_CONV_BAND (read per call): 0 never, 2 the one-addend launches only,
+// PT_CONV_BAND (diagnostic builds only, read per call): 0 never, 2 the one-addend launches only,
 // 1 or unset: always.  First session of r03: k_conv_ba 38.9 -> 37.3 us banded,
 // k_conv_bb 41.9 -> 42.8 us (profiles/r03_ablate_band.txt); with the flat
 // conv pipeline k_conv_bb is equal either way (38.1 us) and the point-wise
 // kernels after it run faster (k_pw_ba 58.5 -> 56.2, k_pw_bb 71.7 -> 69.2 us,
 // interleaved; summed device time per step 23.10 -> 22.80 ms).
-int band_env() {
-  const char* e = getenv("PT_CONV_BAND");
-  return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
-}
+int band_env() { return PT_SW("PT_CONV_BAND", 1); }
 template <class S>
 void launch_conv_bwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   if constexpr (sizeof(S) == 2) {
@@ -3977,35 +3971,20 @@ inline bool syncbn(const pt_cell_dist* dist) { return dist && dist->bn_world > 1
 // The fused forward (k_fused_fa / k_fused_fb) covers the bf16 InT / hGRU cell
 // on single-tile (32x32) frames with k <= 7 and the inhibition branch; other
 // configurations, and PT_CELL_FUSED=0, run the split kernels.
-bool fused_env() {             // read per call: tests A/B the two paths in one process
-  const char* e = getenv("PT_CELL_FUSED");
-  return !(e && e[0] == '0');
-}
+bool fused_env() { return PT_SW("PT_CELL_FUSED", 1) != 0; }   // diag builds: read per call
 // k_pw_bb2 (the half-row backward point-wise B, r04) by default;
-// PT_PWB2=0 (read per call) selects k_pw_bb.
-bool pwb2_env() {
-  const char* e = getenv("PT_PWB2");
-  return !(e && e[0] == '0');
-}
+// PT_PWB2=0 (diagnostic builds only, read per call) selects k_pw_bb.
+bool pwb2_env() { return PT_SW("PT_PWB2", 1) != 0; }
 // k_pw_ba2 (its PR-layout counterpart): opt-in (PT_PWA2=1).  Measured r04
 // (B=256 T=64, interleaved): 59.9-60.1 vs 58.4-58.7 us for k_pw_ba, which
 // already ran one round of workgroups (4 rows per wave); k_pw_bb2's gain came
 // from halving the rounds, not from the layout.
-bool pwa2_env() {
-  const char* e = getenv("PT_PWA2");
-  return e && e[0] == '1';
-}
-// k_wgrad16 (bf16, k = 7) by default; PT_WG16=0 (read per call) selects the
+bool pwa2_env() { return PT_SW("PT_PWA2", 0) == 1; }
+// k_wgrad16 (bf16, k = 7) by default; PT_WG16=0 (diagnostic builds only, read per call) selects the
 // 8-wave k_wgrad.
-bool wg16_env() {
-  const char* e = getenv("PT_WG16");
-  return !(e && e[0] == '0');
-}
+bool wg16_env() { return PT_SW("PT_WG16", 1) != 0; }
 // its LDS-DMA band staging on untiled frames (PT_WGDMA=0: register staging)
-bool wgdma_env() {
-  const char* e = getenv("PT_WGDMA");
-  return !(e && e[0] == '0');
-}
+bool wgdma_env() { return PT_SW("PT_WGDMA", 1) != 0; }
 bool use_fused(const pt_cell_desc* d, const Plan& p) {
   return fused_env() && d->dtype == PT_DTYPE_BF16 && p.ntx * p.nty == 1 &&
          p.K <= 2 * PADMAX + 1 && !d->no_inh;
@@ -4014,10 +3993,7 @@ bool use_fused(const pt_cell_desc* d, const Plan& p) {
 // Persistent forward (k_persist_fwd): opt-in (PT_CELL_PERSIST=1, read per
 // call) on the fused configurations without SyncBN, and only when the B
 // workgroups are all resident at once (occupancy x CUs, checked per device).
-bool persist_env() {
-  const char* e = getenv("PT_CELL_PERSIST");
-  return e && e[0] == '1';
-}
+bool persist_env() { return PT_SW("PT_CELL_PERSIST", 0) == 1; }
 template <class S>
 bool persist_fits(int B) {
   static int cap[2] = {-1, -1};           // per storage type; one device per process
@@ -4079,6 +4055,13 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   ca.wf = a.wf_inh;
   cb.wf = a.wf_exc;
   if (use_fused(d, p) && !syncbn(dist) && persist_env() && persist_fits<S>(p.B)) {
+    // it reads its give-up flag back (a host sync below): illegal under an
+    // outer stream capture, so refuse that case with a clear message
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+      return fail(PT_ERR_UNSUPPORTED,
+                  "the persistent forward (PT_CELL_PERSIST=1, diagnostic build) cannot run under stream capture%s%ld");
     unsigned* done = (unsigned*)((char*)ws + p.o_bnf_done);
     unsigned* err = (unsigned*)((char*)ws + p.o_err);
     timed(PT_K_PERSIST, st, [&] {

@@ -33,6 +33,22 @@
 #endif
 #define PT_ABL(x) (PT_DIAG ? (x) : 0)
 
+// Kernel-variant switches (the A/B experiments of DESIGN.md §9: PT_CELL_FUSED,
+// PT_PWB2, PT_WG16, PT_LCONV_FAST, ...): PT_SW(name, default) reads the
+// environment variable `name` (its first digit) in the diagnostic builds only.
+// The release libraries compile every switch to its default -- the name is not
+// even in the binary -- so the environment cannot change which kernels run.
+#if PT_DIAG
+#include <stdlib.h>
+inline int pt_sw_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && e[0] >= '0' && e[0] <= '9' ? e[0] - '0' : dflt;
+}
+#define PT_SW(name, dflt) pt_sw_env(name, dflt)
+#else
+#define PT_SW(name, dflt) (dflt)
+#endif
+
 namespace ptc {
 
 constexpr int C = 32;          // channels (MFMA tile width)

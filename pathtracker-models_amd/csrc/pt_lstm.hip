@@ -1220,20 +1220,14 @@ LPlan plan(const pt_lstm_desc* d) {
     default: { constexpr int KC = 15; CALL; } break;       \
   }
 
-// PT_LCONV_FAST=0 (read per call) selects k_lconv's plain column loop (A/B test)
-int lconv_fast_env() {
-  const char* e = getenv("PT_LCONV_FAST");
-  return !(e && e[0] == '0');
-}
+// PT_LCONV_FAST=0 (diagnostic builds only, read per call) selects k_lconv's plain column loop (A/B test)
+int lconv_fast_env() { return PT_SW("PT_LCONV_FAST", 1) != 0; }
 // the transposed conv on 8 waves of 4 rows (two per SIMD) instead of 4 of 8:
-// opt-in (PT_LCONVT8=1, read per call).  Measured r04 (cfg3,
+// opt-in (PT_LCONVT8=1, diagnostic builds only, read per call).  Measured r04 (cfg3,
 // profiles/r04_lconvt8_ab.txt): 45.83 vs 45.64 ms per step -- the 256-VGPR
 // budget spills 42 registers and the 8 waves load the same weights twice as
 // often as 4.
-int lconvt8_env() {
-  const char* e = getenv("PT_LCONVT8");
-  return e && e[0] == '1';
-}
+int lconvt8_env() { return PT_SW("PT_LCONVT8", 0) == 1; }
 template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
          hipStream_t st) {
@@ -1261,14 +1255,11 @@ int conv_k(int K, const void* src, const void* wf, float* out, const float* add,
   return rc;
 }
 
-// k_lwgrad2 for bf16 k <= 7: opt-in (PT_LWGRAD2=1, read per call).  Measured
+// k_lwgrad2 for bf16 k <= 7: opt-in (PT_LWGRAD2=1, diagnostic builds only, read per call).  Measured
 // r04 (cfg3, profiles/r04_lwgrad2_ab.txt): 47.56 vs 46.96 ms per step for
 // k_lwgrad -- its 2.3x fewer LDS reads did not pay for the 2.5x taller X band
 // (the K - 1 halo rows) and the D fragments read at every band start.
-int lwgrad2_env() {
-  const char* e = getenv("PT_LWGRAD2");
-  return e && e[0] == '1';
-}
+int lwgrad2_env() { return PT_SW("PT_LWGRAD2", 0) == 1; }
 template <class S, int K>
 int wgrad(const LWgradArgs& a, hipStream_t st) {
   using Bd = LWBand<S, K>;
@@ -1623,6 +1614,10 @@ const char* pt_lstm_last_error(void) { return g_err; }
 #ifndef PT_SRC_HASH
 #define PT_SRC_HASH "unstamped"
 #endif
+#if PT_DIAG
+const char* pt_lstm_version(void) { return "pt_lstm 0.2 gfx950 diag src " PT_SRC_HASH; }
+#else
 const char* pt_lstm_version(void) { return "pt_lstm 0.2 gfx950 src " PT_SRC_HASH; }
+#endif
 
 }  // extern "C"

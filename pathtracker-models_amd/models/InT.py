@@ -6,8 +6,11 @@ tuple and ``state_dict`` keys as the reference (``rCell`` models/InT.py:58-143,
 RNG order, so a given ``torch.manual_seed`` yields the reference's initial
 weights and checkpoints interchange.  What differs is the execution: the
 T-frame recurrence and its BPTT run as hand-written gfx950 kernels behind the
-C-ABI of ``include/pt_cell.h`` (see ``ptamd/cell.py``); only the tiny readout
-(:236-241) stays in PyTorch.
+C-ABI of ``include/pt_cell.h`` (see ``ptamd/cell.py``), and so does the readout
+head (:236-241: ``readout_conv``, the target channel, ``target_conv``, the
+global mean and ``readout_dense`` as one forward and one backward kernel per
+clip, ``include/pt_readout.h`` / ``ptamd/readout.py``); the loss and the
+optimizer stay in PyTorch.
 
 Precision: ``InT.cell_dtype`` selects the cell's storage / MFMA operand type:
 ``'f32'`` (exact-f32 MFMA, the parity path; default, or env PT_CELL_DTYPE) or

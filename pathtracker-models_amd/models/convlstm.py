@@ -184,7 +184,13 @@ class ConvLSTM(nn.Module):
                 states.append(internal_h)
             state_2nd_last = internal_h.detach().requires_grad_()
             state_2nd_last_c = internal_c.detach().requires_grad_()
-            last_state, internal_c = self.unit1(x, state_2nd_last, state_2nd_last_c)
+            # with jacobian_penalty the penalty keeps its graph (create_graph,
+            # reference :158-162, both grad methods): that is a double backward
+            # through the last step, so it runs as torch ops (torch_step), as
+            # the bptt branch's last two steps do
+            graph = self.training and self.jacobian_penalty
+            step = self.unit1.torch_step if graph else self.unit1
+            last_state, internal_c = step(x, state_2nd_last, state_2nd_last_c)
             internal_h = dummyhgru.apply(state_2nd_last, last_state, epoch, itr, self.exp_name,
                                          self.num_iter)
             if testmode:
@@ -192,10 +198,10 @@ class ConvLSTM(nn.Module):
             if self.training:
                 ones = torch.ones_like(last_state)
                 jv = torch.autograd.grad(last_state, state_2nd_last, grad_outputs=[ones],
-                                         retain_graph=True, allow_unused=True)[0]
+                                         retain_graph=True, create_graph=graph, allow_unused=True)[0]
                 jv_penalty = (jv - 0.90).clamp(0) ** 2
                 jv = torch.autograd.grad(internal_c, state_2nd_last_c, grad_outputs=[ones],
-                                         retain_graph=True, allow_unused=True)[0]
+                                         retain_graph=True, create_graph=graph, allow_unused=True)[0]
                 jv_penalty = jv_penalty + (jv - 0.90).clamp(0) ** 2
         elif self.grad_method == 'bptt':
             if self.training and self.timesteps < 2:

@@ -72,8 +72,10 @@ class PtCellError(RuntimeError):
     pass
 
 
-_lock = threading.Lock()
+_lock = threading.RLock()
 _lib = None
+_opened = {}          # path -> CDLL (the release and the diagnostic library may both be open)
+_override = None      # path of the library diag_library() made current, process-wide
 
 
 def use_diag():
@@ -85,17 +87,48 @@ def use_diag():
         LIB_PATH = DIAG_PATH
 
 
+class diag_library:
+    """Context manager: every call into the cell library inside the block goes
+    to the diagnostic build (libptcell_diag.so), opened beside the release one.
+    For the kernel-variant A/B tests, which set PT_CELL_FUSED, PT_PWB2, ... in
+    the environment: only the diagnostic build reads them.  Process-wide (the
+    autograd backward runs on another thread), not re-entrant across threads;
+    the forward and backward of one step must both run inside the block."""
+
+    def __enter__(self):
+        global _override
+        _lock.acquire()
+        self._prev = _override
+        _override = DIAG_PATH
+        return _open(DIAG_PATH)
+
+    def __exit__(self, *exc):
+        global _override
+        _override = self._prev
+        _lock.release()
+        return False
+
+
 def load():
     """Load (once) and return the library; raise if it is not built."""
     global _lib
     with _lock:
-        if _lib is not None:
-            return _lib
-        if not os.path.exists(LIB_PATH):
+        if _override is not None:
+            return _open(_override)
+        if _lib is None:
+            _lib = _open(LIB_PATH)
+        return _lib
+
+
+def _open(path):
+    with _lock:
+        if path in _opened:
+            return _opened[path]
+        if not os.path.exists(path):
             raise PtCellError(
-                f"{LIB_PATH} is missing: build the HIP extension first "
+                f"{path} is missing: build the HIP extension first "
                 "(python __graft_entry__.py build, or python -m ptamd.build)")
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(path)
         lib.pt_cell_saved_bytes.restype = ctypes.c_size_t
         lib.pt_cell_saved_bytes.argtypes = [ctypes.POINTER(Desc)]
         lib.pt_cell_workspace_bytes.restype = ctypes.c_size_t
@@ -127,7 +160,7 @@ def load():
         lib.pt_cell_timing_reset.restype = ctypes.c_int
         lib.pt_last_error.restype = ctypes.c_char_p
         lib.pt_version.restype = ctypes.c_char_p
-        _lib = lib
+        _opened[path] = lib
         return lib
 
 

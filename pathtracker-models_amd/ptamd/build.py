@@ -8,7 +8,10 @@ to the ctypes bindings so they travel with the repository snapshot to the GPU
 box.  ``libptcell_diag.so`` is the same cell library built with -DPT_DIAG=1
 (the PT_CELL_ABLATE / PT_CELL_DEBUG_STOP switches and pt_cell_trace, for
 tools/ only: ``ptamd._lib.use_diag()``); the release ``libptcell.so`` ignores
-those switches.
+those switches; ``libptlstm_diag.so`` is the same for the ConvLSTM library.
+The diagnostic builds also honour the kernel-variant switches (PT_CELL_FUSED,
+PT_PWB2, PT_WG16, PT_LCONV_FAST, ...: ``PT_SW`` in csrc/pt_device.h), which the
+release libraries compile to their defaults.
 """
 from __future__ import annotations
 
@@ -27,13 +30,15 @@ INC = os.path.join(REPO, "include")
 _CELL = ([os.path.join(CSRC, "pt_cell.hip"), os.path.join(CSRC, "pt_readout.hip")],
          [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
           os.path.join(INC, "pt_cell.h"), os.path.join(INC, "pt_readout.h")])
+_LSTM = ([os.path.join(CSRC, "pt_lstm.hip")],
+         [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
+          os.path.join(INC, "pt_lstm.h")])
 LIBS = {
     "libptcell.so": _CELL,
     "libptcell_diag.so": _CELL + (["-DPT_DIAG=1"],),
     "libpttfr.so": ([os.path.join(CSRC, "pt_tfrecord.cpp")], [os.path.join(INC, "pt_tfrecord.h")]),
-    "libptlstm.so": ([os.path.join(CSRC, "pt_lstm.hip")],
-                     [os.path.join(CSRC, "pt_device.h"), os.path.join(CSRC, "pt_graph.h"),
-                      os.path.join(INC, "pt_lstm.h")]),
+    "libptlstm.so": _LSTM,
+    "libptlstm_diag.so": _LSTM + (["-DPT_DIAG=1"],),
 }
 OUT = os.path.join(HERE, "libptcell.so")      # kept for callers of the old single-library API
 # The compiler line of the HIP libraries; part of the source stamp.

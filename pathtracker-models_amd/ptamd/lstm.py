@@ -56,21 +56,55 @@ class PtLstmError(RuntimeError):
     pass
 
 
-_lock = threading.Lock()
+# The diagnostic build (-DPT_DIAG=1): also honours the kernel-variant switches
+# PT_LCONV_FAST / PT_LCONVT8 / PT_LWGRAD2, which libptlstm.so compiles to their
+# defaults; tests A/B the variants through diag_library().
+DIAG_PATH = os.path.join(HERE, "libptlstm_diag.so")
+
+_lock = threading.RLock()
 _lib = None
+_opened = {}
+_override = None
+
+
+class diag_library:
+    """Context manager: calls inside the block go to libptlstm_diag.so
+    (process-wide; see ptamd._lib.diag_library)."""
+
+    def __enter__(self):
+        global _override
+        _lock.acquire()
+        self._prev = _override
+        _override = DIAG_PATH
+        return _open(DIAG_PATH)
+
+    def __exit__(self, *exc):
+        global _override
+        _override = self._prev
+        _lock.release()
+        return False
 
 
 def load():
     """Load (once) and return the library; raise if it is not built."""
     global _lib
     with _lock:
-        if _lib is not None:
-            return _lib
-        if not os.path.exists(LIB_PATH):
+        if _override is not None:
+            return _open(_override)
+        if _lib is None:
+            _lib = _open(LIB_PATH)
+        return _lib
+
+
+def _open(path):
+    with _lock:
+        if path in _opened:
+            return _opened[path]
+        if not os.path.exists(path):
             raise PtLstmError(
-                f"{LIB_PATH} is missing: build the HIP extensions first "
+                f"{path} is missing: build the HIP extensions first "
                 "(python __graft_entry__.py build, or python -m ptamd.build)")
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(path)
         D = ctypes.POINTER(Desc)
         lib.pt_lstm_saved_bytes.restype = ctypes.c_size_t
         lib.pt_lstm_saved_bytes.argtypes = [D]
@@ -93,7 +127,7 @@ def load():
         lib.pt_lstm_stem_backward.argtypes = [_P, _i, _P, _P, _P, _i, _i, _i, _ll, _P, _P, _P, _P]
         lib.pt_lstm_last_error.restype = ctypes.c_char_p
         lib.pt_lstm_version.restype = ctypes.c_char_p
-        _lib = lib
+        _opened[path] = lib
         return lib
 
 

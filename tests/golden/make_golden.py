@@ -200,16 +200,19 @@ def make_r3d(ref_r3d, tag, *, batch, t_len, seed=0):
     print(tag, "loss", float(out["loss"]))
 
 
-def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0, jacobian_penalty=False):
+def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0, jacobian_penalty=False,
+                  grad_method="bptt", num_iter=50):
     """jacobian_penalty=True: the penalty is built with create_graph
     (convlstm.py:158-162) and the training loss is loss + 10 mean(jv_penalty),
-    as mainclean.py:191-195 forms it; the grads are those of that sum."""
+    as mainclean.py:191-195 forms it; the grads are those of that sum.
+    grad_method='rbp': the no-grad unroll, the last step with grad and the
+    Neumann-series backward (dummyhgru, convlstm.py:9-53, :124-135)."""
     torch.manual_seed(3000 + seed)
     cwd = os.getcwd()
     os.chdir(REF)                     # gabor_serre.npy is opened relative to CWD (convlstm.py:105)
     try:
-        model = ref_clstm.ConvLSTM(timesteps=timesteps, filt_size=filt,
-                                   jacobian_penalty=jacobian_penalty)
+        model = ref_clstm.ConvLSTM(timesteps=timesteps, filt_size=filt, num_iter=num_iter,
+                                   jacobian_penalty=jacobian_penalty, grad_method=grad_method)
     finally:
         os.chdir(cwd)
     g = torch.Generator().manual_seed(seed)
@@ -237,7 +240,8 @@ def make_convlstm(ref_clstm, tag, *, batch, timesteps, filt, seed=0, jacobian_pe
         if p.grad is not None:
             out["grad." + name] = p.grad.numpy().copy()
     out.update(img=img.numpy(), target=target.numpy(), cfg_timesteps=np.array(timesteps),
-               cfg_filt=np.array(filt), cfg_jacobian_penalty=np.array(int(jacobian_penalty)))
+               cfg_filt=np.array(filt), cfg_jacobian_penalty=np.array(int(jacobian_penalty)),
+               cfg_rbp=np.array(int(grad_method == "rbp")), cfg_num_iter=np.array(num_iter))
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
     print(tag, "loss", float(out["loss"]))
 
@@ -343,6 +347,12 @@ def main():
             "convlstm_jvp_t2": lambda: make_convlstm(ref_clstm, "convlstm_jvp_t2", batch=2,
                                                      timesteps=2, filt=5, seed=18,
                                                      jacobian_penalty=True),
+            # grad_method='rbp' with the penalty's graph (create_graph applies to
+            # both grad methods, convlstm.py:158-162)
+            "convlstm_rbp_jvp": lambda: make_convlstm(ref_clstm, "convlstm_rbp_jvp", batch=2,
+                                                      timesteps=4, filt=7, seed=19,
+                                                      jacobian_penalty=True, grad_method="rbp",
+                                                      num_iter=5),
         }
         only = os.environ.get("GOLDEN_ONLY")          # comma-separated tags to (re)generate
         for tag, job in jobs.items():

@@ -57,3 +57,22 @@ def test_pmc_traffic_needs_matching_library_stamp(tmp_path, monkeypatch):
     assert bench.pmc_traffic("k_pw_bb", 256, 64, "bf16", "pt_cell x src abc") == 123
     assert bench.pmc_traffic("k_pw_bb", 256, 64, "bf16", "pt_cell x src def") is None
     assert bench.pmc_traffic("k_pw_bb", 128, 64, "bf16", "pt_cell x src abc") is None
+
+
+def test_roofline_follows_survey_8d():
+    """bench.py reports the dominant kernel against the roofline SURVEY.md §8(d)
+    binds it to (MFMA for every kernel with a k x k conv), the step's §8(d)
+    FLOPs (41.91 GFLOP per 64-frame clip) and the PMC step bytes against
+    §8(d)'s 17.2 MB-per-clip minimum; the r04 numbers reproduce from the
+    committed profiles (0.173 of MFMA for k_fused_fa, 66.1 GB/step)."""
+    import bench
+    assert abs(bench.step_flops_8d(1, 64) - 41.91e9) < 0.01e9
+    r, fl, by, avg = bench.kernel_roofline("k_fused_fa", 65.86e-3 * 640, 640, 256, 64, 10, "bf16", 4, True)
+    assert r["bound"] == "mfma" and fl == 256 * (bench.conv_flops() + 4 * bench.gate_flops())
+    assert abs(r["frac"] - 0.1728) < 1e-3 and r["frac"] == r["mfma_frac"]
+    r, *_ = bench.kernel_roofline("k_pw_ba", 57e-3 * 640, 640, 256, 64, 10, "bf16", 4, True)
+    assert r["bound"] == "hbm"
+    sb = bench.pmc_step_bytes(256, 64, "bf16", "pt_cell 0.2 gfx950 src 0fc1382ba8c5")
+    assert sb is not None and abs(sb / 1e9 - 66.15) < 0.1
+    assert abs(sb / (256 * 64 * bench.BYTES_8D_FRAME) - 15.0) < 0.1
+    assert bench.pmc_step_bytes(256, 64, "bf16", "some other library") is None

@@ -4,18 +4,17 @@ frames) against the split kernels (k_pw_fa, k_conv_fwd, k_pw_fb, k_conv_fwd):
 the arithmetic is the same operation for operation (the LDS tile holds the
 bf16 values the split conv would load), so logits, per-frame testmode outputs
 and every gradient must agree bit for bit.  PT_CELL_FUSED=0 selects the split
-path (read per call by the library).
+path (read per call by the diagnostic library: tests/variants.py).
 
 The persistent forward (k_persist_fwd, PT_CELL_PERSIST=1: all T frames of the
 fused segments in one launch, the BatchNorm syncs as in-launch waits on the
 deterministic group sums) is the same arithmetic in the same reduction order,
 so it too must reproduce the per-segment launches bit for bit.  So must the
 banded backward conv (PT_CONV_BAND=1): per output row the same MFMA order."""
-import os
-
 import pytest
 import torch
 import torch.nn.functional as F
+from variants import variants
 
 pytestmark = pytest.mark.gpu
 
@@ -27,10 +26,7 @@ def _dev():
 
 
 def _run(m, x, y, fused, persist=False, band=False):
-    os.environ["PT_CELL_FUSED"] = str(int(fused))
-    os.environ["PT_CELL_PERSIST"] = "1" if persist else "0"
-    os.environ["PT_CONV_BAND"] = "1" if band else "0"
-    try:
+    with variants(PT_CELL_FUSED=int(fused), PT_CELL_PERSIST=int(persist), PT_CONV_BAND=int(band)):
         m.zero_grad(set_to_none=True)
         out, _ = m(x)
         F.binary_cross_entropy_with_logits(out, y.reshape(-1, 1)).backward()
@@ -39,10 +35,6 @@ def _run(m, x, y, fused, persist=False, band=False):
         torch.cuda.synchronize()
         return (out.detach().clone(), states.clone(), gates.clone(),
                 {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None})
-    finally:
-        os.environ.pop("PT_CELL_FUSED", None)
-        os.environ.pop("PT_CELL_PERSIST", None)
-        os.environ.pop("PT_CONV_BAND", None)
 
 
 @pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("int", "tanh", 5, 3),

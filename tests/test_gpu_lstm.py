@@ -75,17 +75,21 @@ def test_convlstm_bptt_grads_and_jv_f32(tag):
         _assert_close(f"grad {k}", got[k].cpu(), v, 1e-6, 1e-3)
 
 
-@pytest.mark.parametrize("tag", ["convlstm_jvp", "convlstm_jvp_t2"])
+@pytest.mark.parametrize("tag", ["convlstm_jvp", "convlstm_jvp_t2", "convlstm_rbp_jvp"])
 def test_convlstm_jacobian_penalty_with_graph_f32(tag):
     """jacobian_penalty=True: the penalty carries its graph (convlstm.py:158-162)
     and the loss is loss + 10 mean(jv_penalty) (mainclean.py:191-195); the
     reference's gradients of that sum within 1e-3 (golden from the reference
-    with the flag set)."""
+    with the flag set).  convlstm_rbp_jvp: the same with grad_method='rbp'
+    (create_graph applies to both methods; the Neumann-series backward of
+    dummyhgru, 5 terms)."""
     from models import convlstm as cl
     dev = _dev()
     g = load(tag)
+    rbp = "cfg_rbp" in g and int(g["cfg_rbp"]) == 1
     m = cl.ConvLSTM(timesteps=int(g["cfg_timesteps"]), filt_size=int(g["cfg_filt"]),
-                    jacobian_penalty=True)
+                    jacobian_penalty=True, grad_method="rbp" if rbp else "bptt",
+                    num_iter=int(g["cfg_num_iter"]) if rbp else 50)
     m.load_state_dict(params(g), strict=True)
     m = m.to(dev).train()
     img = torch.from_numpy(g["img"]).to(dev)
@@ -101,6 +105,46 @@ def test_convlstm_jacobian_penalty_with_graph_f32(tag):
     assert set(got) == set(ref), set(got) ^ set(ref)
     for k, v in ref.items():
         _assert_close(f"grad {k}", got[k].cpu(), v, 1e-6, 1e-3)
+
+
+def test_convlstm_jacobian_penalty_bf16_vs_f32():
+    """jacobian_penalty=True with the bf16 cell: the library's first T-2 steps
+    store bf16 states, which feed the last two steps' f32 torch ops and their
+    double backward.  Against the f32 run (itself pinned to the reference
+    golden above): the penalty within 5 % relative RMS, the output within 3 %
+    (bf16 tolerance of test_convlstm_bf16_tolerance), gradient cosine > 0.95
+    per tensor; measured values recorded (gpurun_out/parity_records.json)."""
+    from goldens import record
+    from models import convlstm as cl
+    dev = _dev()
+    g = load("convlstm_jvp")
+    img = torch.from_numpy(g["img"]).to(dev)
+    tgt = torch.from_numpy(g["target"]).to(dev)
+    res = {}
+    for dt in ("f32", "bf16"):
+        m = cl.ConvLSTM(timesteps=int(g["cfg_timesteps"]), filt_size=int(g["cfg_filt"]),
+                        jacobian_penalty=True)
+        m.load_state_dict(params(g), strict=True)
+        m = m.to(dev).train()
+        m.cell_dtype = dt
+        out, jv, loss = m(img, 0, 0, tgt, torch.nn.CrossEntropyLoss())
+        assert jv.requires_grad
+        (loss + jv.mean() * 1e1).backward()
+        res[dt] = (out.detach().double().cpu(), jv.detach().double().cpu(),
+                   {k: p.grad.detach().double().flatten().cpu() for k, p in m.named_parameters()
+                    if p.grad is not None})
+    (o32, j32, g32), (o16, j16, g16) = res["f32"], res["bf16"]
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-30))
+    worst = 1.0
+    for k in g32:
+        if g32[k].norm() > 0:
+            cos = float(g16[k] @ g32[k] / (g16[k].norm() * g32[k].norm()))
+            worst = min(worst, cos)
+            assert cos > 0.95, (k, cos)
+    record("convlstm_jvp_bf16_vs_f32", {"penalty_rel_rms": rel(j16, j32), "output_rel_rms": rel(o16, o32),
+                                        "min_grad_cos": worst})
+    assert rel(j16, j32) < 5e-2, rel(j16, j32)
+    assert rel(o16, o32) < 3e-2, rel(o16, o32)
 
 
 def test_convlstm_bf16_tolerance():

@@ -89,7 +89,7 @@ def test_lconv_prefetch_loop_is_bitwise_the_plain_loop(switch):
     8-wave transposed conv (PT_LCONVT8=1), each against the default.
     Same MFMA order per accumulator, so logits, the Jacobian penalty and every
     gradient are bitwise equal (k=7, 5 and 3)."""
-    import os
+    from variants import variants
     dev = _dev()
     for k in (7, 5, 3):
         m = _model(k, 11 + k).to(dev).train()
@@ -97,21 +97,14 @@ def test_lconv_prefetch_loop_is_bitwise_the_plain_loop(switch):
         x, y = _clips(13 + k, 6, 5)
         x, y = x.to(dev), y.to(dev).reshape(-1, 1)
         res = []
-        old = os.environ.get(switch)
-        try:
-            for v in ("0", "1"):
-                os.environ[switch] = v
+        for v in ("0", "1"):
+            with variants(**{switch: v}):          # the diagnostic library reads the switch
                 m.zero_grad(set_to_none=True)
                 out, jv = m(x)
                 F.binary_cross_entropy_with_logits(out, y).backward()
                 torch.cuda.synchronize()
                 res.append((out.detach().clone(), jv.detach().clone(),
                             {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
-        finally:
-            if old is None:
-                os.environ.pop(switch, None)
-            else:
-                os.environ[switch] = old
         (o0, j0, g0), (o1, j1, g1) = res
         assert torch.equal(o0, o1) and torch.equal(j0, j1), k
         for n in g0:

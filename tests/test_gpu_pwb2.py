@@ -4,12 +4,13 @@ one process: every parameter
 gradient of one forward + backward, f32 (different summation order only:
 1e-5 relative) and bf16 (its own rounding of the 1x1 gate and weight-gradient
 operands: gradient cosine), for InT, InT no_inh and hGRU.  The reference
-goldens (test_gpu_parity.py) run k_pw_bb2 too: it is the default."""
-import os
-
+goldens (test_gpu_parity.py) run k_pw_bb2 too: it is the default.  Both
+sides run on the diagnostic library, which reads the switches
+(tests/variants.py)."""
 import pytest
 import torch
 import torch.nn.functional as F
+from variants import variants
 
 pytestmark = pytest.mark.gpu
 
@@ -47,21 +48,10 @@ def test_pwb2_matches_pwb(kind, dtype):
     m = m.to(dev)
     m.cell_dtype = dtype
     x, y = bench.make_data(77, 24, t, dev)
-    keys = ("PT_PWB2", "PT_PWA2")
-    old = {k: os.environ.get(k) for k in keys}
-    try:
-        for k in keys:
-            os.environ[k] = "0"
+    with variants(PT_PWB2=0, PT_PWA2=0):
         g0 = _grads(m, x, y)
-        for k in keys:
-            os.environ[k] = "1"
+    with variants(PT_PWB2=1, PT_PWA2=1):
         g1 = _grads(m, x, y)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
     assert g0.keys() == g1.keys()
     for k in g0:
         a, b = g1[k], g0[k]

@@ -44,23 +44,41 @@ def _setup():
     return run
 
 
+# every switch at a non-default value (phase-skipping ablations, a debug stop
+# and the kernel-variant A/B switches)
+NON_DEFAULT = dict(PT_CELL_ABLATE=str(1 | 4 | 8 | 32 | 512), PT_CELL_DEBUG_STOP="2",
+                   PT_CELL_FUSED="0", PT_PWB2="0", PT_PWA2="1", PT_WG16="0", PT_WGDMA="0",
+                   PT_CELL_PERSIST="1", PT_XCD_MAP="0", PT_CONV_BAND="0")
+
+
 def test_release_library_ignores_the_diagnostic_switches():
+    """With every diagnostic and kernel-variant switch set to a non-default
+    value the release library's forward and backward are bit-identical to a
+    run without them; and the diagnostic build at its defaults equals the
+    release library bit for bit (so the A/B tests, which compare variants on
+    the diagnostic build, compare against the release kernels)."""
     from ptamd import _lib
     run = _setup()
     lib = _lib.load()
     assert "diag" not in lib.pt_version().decode()
     o0, g0 = run()
-    os.environ.update(PT_CELL_ABLATE=str(1 | 4 | 8 | 32 | 512), PT_CELL_DEBUG_STOP="2")
+    os.environ.update(NON_DEFAULT)
     try:
         o1, g1 = run()
     finally:
-        os.environ.pop("PT_CELL_ABLATE")
-        os.environ.pop("PT_CELL_DEBUG_STOP")
+        for k in NON_DEFAULT:
+            os.environ.pop(k)
     assert torch.equal(o0, o1)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
     assert lib.pt_cell_trace(None, -1) == 2                  # PT_ERR_UNSUPPORTED
     assert b"diagnostic build" in lib.pt_last_error()
+    with _lib.diag_library() as dl:
+        assert "diag" in dl.pt_version().decode()
+        o2, g2 = run()
+    assert torch.equal(o0, o2)
+    for k in g0:
+        assert torch.equal(g0[k], g2[k]), ("diag build at its defaults", k)
 
 
 _CHILD = r"""

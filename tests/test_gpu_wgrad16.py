@@ -8,12 +8,11 @@ is bitwise equal.  Also: two runs of the default are bitwise equal, the
 LDS-DMA band staging (default on untiled frames) equals the register staging
 (PT_WGDMA=0) bitwise, also on 64x64 (tiled) hGRU frames, whose X halo rows
 and columns come from the neighbouring tiles."""
-import os
-
 import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
+from variants import variants
 
 pytestmark = pytest.mark.gpu
 
@@ -27,15 +26,9 @@ def _grads(m, x, y):
 
 
 def _with_env(key, val, fn):
-    old = os.environ.get(key)
-    os.environ[key] = val
-    try:
+    """fn() on the diagnostic library with switch key = val (tests/variants.py)."""
+    with variants(**{key: val}):
         return fn()
-    finally:
-        if old is None:
-            os.environ.pop(key, None)
-        else:
-            os.environ[key] = old
 
 
 @pytest.mark.parametrize("kind", ["int", "int_noinh", "hgru", "hgru64"])
@@ -107,7 +100,7 @@ def test_wgrad16_smallest_shapes(kind, b, t):
     x = torch.from_numpy(np.ascontiguousarray(clips.transpose(0, 4, 1, 2, 3), dtype=np.float32) / 255.0).to(dev)
     y = torch.tensor([ord(v) for v in labels], dtype=torch.float32, device=dev)
     g8 = _with_env("PT_WG16", "0", lambda: _grads(m, x, y))
-    g16 = _grads(m, x, y)
+    g16 = _with_env("PT_WG16", "1", lambda: _grads(m, x, y))
     greg = _with_env("PT_WGDMA", "0", lambda: _grads(m, x, y))
     for k in g8:
         a, ref = g16[k], g8[k]
