@@ -449,6 +449,14 @@ struct CellArgs {
   // f32: I itself).
   float* I;
   S* Ic;
+  // bf16 cell (r05): E and I are stored as two 16-bit planes each instead of
+  // f32 + a bf16 copy -- hi = the value rounded half-up to bf16 (Eh; Ih IS Ic,
+  // the exc conv's input and k_wgrad's X operand) and lo = the low 16 bits of
+  // (f32 bits - hi << 16), so hi + lo restores the f32 value EXACTLY (ldE /
+  // ldI) while a reader that only needs the bf16 value reads half the bytes
+  // (ldEh / ldIh).  f32 cell: E and I above, these null.
+  S* Eh;
+  uint16_t *El, *Il;
   S *gE, *ci, *ce, *eg;
   S* at;                                // hGRU only: attention map per frame (the gated inhibition)
   float* bnstat;                        // [T][4][32] mean0, rstd0, mean1, rstd1
@@ -523,6 +531,129 @@ __host__ __device__ inline BnSlot bnb_slot(const CellArgs<S>& a, int t, int bn, 
           nprod};
 }
 __device__ __forceinline__ size_t clip_off(int b) { return (size_t)b * NPIX * C; }
+
+// ------------------------------------------------------ the f32 states E, I
+// (CellArgs::Eh / El / Il).  Split: hi = (bits + 0x8000) >> 16 (rounded half
+// up in magnitude), lo = bits - (hi << 16) as 16 bits, in [-0x8000, 0x7fff]:
+// bits = (hi << 16) + sext(lo) exactly.  The bf16 MFMA operands taken from E
+// and I in the forward are rounded the same way (op_round), so the hi plane
+// the backward reads is the operand the forward used.
+__device__ __forceinline__ uint32_t split_hi(float v) { return (__float_as_uint(v) + 0x8000u) >> 16; }
+__device__ __forceinline__ float hi_f(float v) { return __uint_as_float(split_hi(v) << 16); }
+template <class S>
+__device__ __forceinline__ f32x16 op_round(const f32x16& v) {
+  if constexpr (sizeof(S) == 4) {
+    return v;
+  } else {
+    f32x16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = hi_f(v[r]);
+    return o;
+  }
+}
+// CL row tile of a split state (4-B loads of the channel pair, as load_cl)
+__device__ __forceinline__ f32x16 load_cl_split(const bf16_t* __restrict__ hi, const uint16_t* __restrict__ lo,
+                                                int c, int h) {
+  const uint32_t* wh = (const uint32_t*)(hi + (c & ~1));
+  const uint32_t* wl = (const uint32_t*)(lo + (c & ~1));
+  const uint32_t sel = bf16_sel(c);
+  const int sh = (c & 1) ? 0 : 16;
+  f32x16 v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint32_t x = wh[cl_x(r, h) * (C / 2)], y = wl[cl_x(r, h) * (C / 2)];
+    v[r] = __uint_as_float(__builtin_amdgcn_perm(x, x, sel) + (uint32_t)((int32_t)(y << sh) >> 16));
+  }
+  return v;
+}
+__device__ __forceinline__ void store_cl_split(bf16_t* __restrict__ hi, uint16_t* __restrict__ lo, int c, int h,
+                                               const f32x16& v) {
+  uint16_t* hp = (uint16_t*)hi;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint32_t b = __float_as_uint(v[r]), hh = (b + 0x8000u) >> 16;
+    hp[cl_x(r, h) * C + c] = (uint16_t)hh;
+    lo[cl_x(r, h) * C + c] = (uint16_t)(b - (hh << 16));
+  }
+}
+// PR (pt_pr.h) half-row tile of a split state: the lane's channel pair is one
+// dword per plane
+__device__ __forceinline__ f32x8 pr_load_split(const bf16_t* __restrict__ hseg, const uint16_t* __restrict__ lseg,
+                                               int lane) {
+  const int n = lane & 15, g = lane >> 4;
+  const uint32_t* wh = (const uint32_t*)hseg + (4 * g) * (C / 2) + n;
+  const uint32_t* wl = (const uint32_t*)lseg + (4 * g) * (C / 2) + n;
+  f32x8 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = wh[i * (C / 2)], y = wl[i * (C / 2)];
+    v[i] = __uint_as_float((x << 16) + (uint32_t)((int32_t)(y << 16) >> 16));
+    v[4 + i] = __uint_as_float((x & 0xffff0000u) + (uint32_t)((int32_t)y >> 16));
+  }
+  return v;
+}
+// E_t / I_t of row offset ro: full precision (ld*), the bf16 operand value
+// (ld*h: the hi plane; the f32 cell reads its f32 array either way), stores
+template <class S>
+__device__ __forceinline__ f32x16 ldE(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return load_cl_split(a.Eh + o, a.El + o, c, h);
+  else return load_cl(a.E + o, c, h);
+}
+template <class S>
+__device__ __forceinline__ f32x16 ldEh(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return load_cl(a.Eh + o, c, h);
+  else return load_cl(a.E + o, c, h);
+}
+template <class S>
+__device__ __forceinline__ f32x16 ldI(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return load_cl_split(a.Ic + o, a.Il + o, c, h);
+  else return load_cl(a.I + o, c, h);
+}
+template <class S>
+__device__ __forceinline__ f32x16 ldIh(const CellArgs<S>& a, int t, size_t ro, int c, int h) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return load_cl(a.Ic + o, c, h);
+  else return load_cl(a.I + o, c, h);
+}
+template <class S>
+__device__ __forceinline__ void stE(const CellArgs<S>& a, int t, size_t ro, int c, int h, const f32x16& v) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) store_cl_split(a.Eh + o, a.El + o, c, h, v);
+  else store_cl(a.E + o, c, h, v);
+}
+template <class S>
+__device__ __forceinline__ void stI(const CellArgs<S>& a, int t, size_t ro, int c, int h, const f32x16& v) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) store_cl_split(a.Ic + o, a.Il + o, c, h, v);
+  else store_cl(a.I + o, c, h, v);
+}
+template <class S>
+__device__ __forceinline__ f32x8 prE(const CellArgs<S>& a, int t, size_t ro, int lane) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return pr_load_split(a.Eh + o, a.El + o, lane);
+  else return pr_load<float>(a.E + o, lane);
+}
+template <class S>
+__device__ __forceinline__ f32x8 prEh(const CellArgs<S>& a, int t, size_t ro, int lane) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return pr_load<S>(a.Eh + o, lane);
+  else return pr_load<float>(a.E + o, lane);
+}
+template <class S>
+__device__ __forceinline__ f32x8 prI(const CellArgs<S>& a, int t, size_t ro, int lane) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return pr_load_split(a.Ic + o, a.Il + o, lane);
+  else return pr_load<float>(a.I + o, lane);
+}
+template <class S>
+__device__ __forceinline__ f32x8 prIh(const CellArgs<S>& a, int t, size_t ro, int lane) {
+  const size_t o = fr_off(t, a.B) + ro;
+  if constexpr (sizeof(S) == 2) return pr_load<S>(a.Ic + o, lane);
+  else return pr_load<float>(a.I + o, lane);
+}
 
 // Spatial tiling.  A frame larger than 32x32 (H, W multiples of 32) is held as
 // nty x ntx tiles of 32x32, each stored and processed like a clip of its own
@@ -1234,6 +1365,48 @@ __device__ __forceinline__ PLds pcarve_bb(char* smem) {
   l.slabl = (float*)p - PWB_SLAB_LO;
   return l;
 }
+// k_pw_ba's layout.  bf16 (r05): the a_w / a_u weight gradients are formed
+// from operand tiles staged channel-major in LDS (CL rows -> [ch][128 px], the
+// PR weight-gradient contraction of pt_pr.h) by one wave per (gate, output
+// half) per set of 4 rows, accumulated in registers and added into the slab
+// once at the end -- instead of two per-row cross-wave LDS reductions (4
+// barriers a row) into a gacc tile; the slab copy holds only the per-channel
+// block.  f32: pcarve (gacc).
+#ifndef PT_PWA_STAGE
+#define PT_PWA_STAGE 1      // 0: the r04 per-row gacc reductions (A/B builds, tools/libab.py)
+#endif
+constexpr int PWA_NPX = PW_NW * IMG;            // pixels per set (one row per wave)
+template <class S>
+constexpr int pwa_lds_bytes() {
+  return sizeof(S) == 2 && PT_PWA_STAGE
+             ? PW_NW * PWA_RPP * IMG * 16 /*xs*/ + PW_NW * SCR_FLOATS * 4 /*scr*/ + 128 * 4 /*stat*/ +
+                   PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ + 3 * stg_bytes<S, PWA_NPX>() /*stage*/ +
+                   NSMALL * 32 * 4 /*slab copy: per-channel block*/
+             : pw_lds_bytes<PWA_RPP, true>();
+}
+template <class S>
+__device__ __forceinline__ PLds pcarve_ba(char* smem) {
+  PLds l = pcarve<PWA_RPP>(smem);
+  if constexpr (sizeof(S) == 2 && PT_PWA_STAGE) {
+    char* p = (char*)(l.red + 512);
+    l.stage = (bf16x8*)p;
+    l.gacc = nullptr;
+    p += 3 * stg_bytes<S, PWA_NPX>();
+    l.slabl = (float*)p - SLAB_G;
+  }
+  return l;
+}
+// A CL row tile (lane = channel c, half h; 16 pixels in 4 runs of 4) into a
+// channel-major stage [ch][NPX + pad] at pixel offset px0, as bf16.
+template <int NPX>
+__device__ __forceinline__ void cl_stage(bf16_t* __restrict__ stg, const f32x16& v, int px0, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  bf16_t* row = stg + c * stg_stride<bf16_t, NPX>() + px0 + 4 * h;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    *(u32x2*)(row + 8 * k) = u32x2{pk_bf16(v[4 * k], v[4 * k + 1]), pk_bf16(v[4 * k + 2], v[4 * k + 3])};
+}
+
 // bf16 1x1 weight gradients without the per-row cross-wave reductions: every
 // wave parks its row's operand tile (CL registers packed as the bf16 MFMA
 // fragments of wgrad_cl) in a slot; after a barrier ONE wave contracts the
@@ -1395,8 +1568,11 @@ __device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, int t, size_t r
   FaIn<S> w;
   w.Iv = zero16(); w.Eo = zero16(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
   if (t > 0) {
-    w.Iv = load_cl(a.I + (t - 1) * fs + ro, c, h);
-    if (t >= 2) w.Eo = load_cl(a.E + (t - 2) * fs + ro, c, h);
+    // I_{t-1} feeds kappa I + gamma and the e_w gate operand: the bf16 cell
+    // reads its hi plane only (r05); E_{t-2} feeds the E update
+    // and is read in full precision
+    w.Iv = ldIh(a, t - 1, ro, c, h);
+    if (t >= 2) w.Eo = ldE(a, t - 2, ro, c, h);
     w.egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
     w.cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
   }
@@ -1440,14 +1616,15 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
     if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 2048))
 #pragma unroll
       for (int r = 0; r < 16; ++r) Ep[r] = (float)(bf16_t)Ep[r];
-    store_cl(a.E + (t - 1) * fs + ro, c, h, Ep);
+    stE(a, t - 1, ro, c, h, Ep);
   }
   if (t == T) return;
+  const f32x16 Eop = op_round<S>(Ep);      // E_{t-1} as the gates' bf16 operand (= its hi plane)
   f32x16 z, xv;
   stem_cl<ACT>(xs, yl, h, st, z, xv);
   F pax[Tr<S>::KS], pae[Tr<S>::KS];
   cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
-  cl_to_pa<S>(wscr, Ep, lane, pae, RND_G(a));
+  cl_to_pa<S>(wscr, Eop, lane, pae, RND_G(a));
   f32x16 acc = zero16();
   acc = gemm_pa<S>(pax, a.gf[0], acc, lane);
   acc = gemm_pa<S>(pae, a.gf[1], acc, lane);
@@ -1473,7 +1650,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
     store_cl(a.at + t * fs + ro, c, h, att);
     cl_to_pa<S>(wscr, att, lane, pai, RND_G(a));
   } else if (a.no_inh) {
-    cl_to_pa<S>(wscr, Ep, lane, pai, RND_G(a));
+    cl_to_pa<S>(wscr, Eop, lane, pai, RND_G(a));
   } else {
     cl_to_pa<S>(wscr, in.Iv, lane, pai, RND_G(a));
   }
@@ -1528,7 +1705,7 @@ __device__ __forceinline__ FbIn<S> fb_load(const CellArgs<S>& a, int t, size_t r
   const size_t fs = fr_off(1, a.B);
   FbIn<S> w;
   w.civ = load_pk(a.ci + t * fs + ro, c, h);
-  w.Iv = t > 0 ? load_cl(a.I + (t - 1) * fs + ro, c, h) : zero16();
+  w.Iv = t > 0 ? ldI(a, t - 1, ro, c, h) : zero16();     // full precision: the I update
   if constexpr (HG) w.gi = load_pk(a.at + t * fs + ro, c, h);   // gated inhibition att_t
   else w.gi = zero_pk<S>();                                     // InT: I_{t-1} (Iv, f32)
   return w;
@@ -1572,9 +1749,8 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float*
   if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 4096))
 #pragma unroll
     for (int r = 0; r < 16; ++r) In[r] = (float)(bf16_t)In[r];
-  store_cl(a.I + t * fs + ro, c, h, In);
-  if constexpr (sizeof(S) == 2) store_cl(a.Ic + t * fs + ro, c, h, In);
-  if (tile) tile_put_cl(tile, y, c, h, In);
+  stI(a, t, ro, c, h, In);                 // bf16: the hi plane is Ic, the exc conv's input
+  if (tile) tile_put_cl(tile, y, c, h, op_round<S>(In));
 }
 
 template <class S, int ACT, int HG>
@@ -1597,8 +1773,7 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
       f32x16 v;
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = (float)g[r];
-      store_cl(a.I + t * fs + ro, c, h, v);
-      if constexpr (sizeof(S) == 2) store_cl(a.Ic + t * fs + ro, c, h, v);
+      stI(a, t, ro, c, h, v);
     }
     return;
   }
@@ -1801,7 +1976,8 @@ __global__ __launch_bounds__(CONV_NT, 1) void k_persist_fwd(const CellArgs<S> a,
 template <class S, int ACT, int HG, int RPP>
 __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int b, int part) {
   using F = typename Tr<S>::frag;
-  const PLds L = pcarve<RPP>(smem);
+  constexpr bool BF = sizeof(S) == 2 && PT_PWA_STAGE;   // staged wave-per-tile 1x1 weight gradients (pcarve_ba)
+  const PLds L = pcarve_ba<S>(smem);
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = a.t, T = a.T, B = a.B;
@@ -1813,10 +1989,20 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   float* slab_p = a.slab + ((size_t)b * PW_PARTS + part) * SLAB;
 
   PT_TR(a, PT_K_PW_BA, 0);
-  slab_prefetch(slab_p, L.slabl, 0, 2, wave, lane);        // a_w, a_u
+  if constexpr (BF) slab_range(slab_p, L.slabl, SLAB_G, NSMALL * 32, wave, lane);   // per-channel block
+  else slab_prefetch(slab_p, L.slabl, 0, 2, wave, lane);                           // a_w, a_u
   if (tail) stage_x(a.x, a.xu8, L.xs, b, tt, T, y0, PW_NW * RPP, tid, PW_NT, a.ntx, a.nty);
-  gacc_zero(L.gacc, 2, tid);
+  if constexpr (!BF) gacc_zero(L.gacc, 2, tid);
   __syncthreads();
+  // BF: wave w forms output half mt = w & 1 of gate gi = w >> 1 (a_w: X = xbn,
+  // a_u: X = E_t) over each set's staged 128 pixels
+  const bool att_wg = tail && (head || HG) && !(PT_ABL(a.ablate) & 16);
+  const int gi = wave >> 1, mt = wave & 1;
+  f32x4 wacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  constexpr int SE = stg_bytes<S, PWA_NPX>() / (int)sizeof(S);
+  S* st_dap = (S*)L.stage;
+  S* st_xv = st_dap + SE;
+  S* st_E = st_dap + 2 * SE;
   PT_TR(a, PT_K_PW_BA, 2);
 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
@@ -1847,7 +2033,8 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
       if (head || HG) {
         const f32x16 dgE = head ? load_cl(dgsrc + ro, c, h) : zero16();
         const Pk<S> dAt = HG ? load_pk(a.dAt + ro, c, h) : zero_pk<S>();
-        const f32x16 Et = head ? load_cl(a.E + t * fs + ro, c, h) : zero16();
+        // E_t as the a_u gate operand and in d att = dgE E_t: the hi plane (bf16 cell)
+        const f32x16 Et = head ? ldEh(a, t, ro, c, h) : zero16();
         F pax[Tr<S>::KS], pae[Tr<S>::KS];
         cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
         cl_to_pa<S>(wscr, Et, lane, pae, RND_G(a));
@@ -1862,8 +2049,16 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
           dap[r] = datt * att[r] * (1.f - att[r]);
           sm[0] += dap[r];
         }
-        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
-        if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
+        if constexpr (BF) {
+          if (att_wg) {             // this set's operands; contracted after the barrier below
+            cl_stage<PWA_NPX>((bf16_t*)st_dap, dap, wave * IMG, lane);
+            cl_stage<PWA_NPX>((bf16_t*)st_xv, xv, wave * IMG, lane);
+            cl_stage<PWA_NPX>((bf16_t*)st_E, Et, wave * IMG, lane);
+          }
+        } else {
+          if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 0 * 1024, L.flush, dap, xv, lane, wave, tid);
+          if (!(PT_ABL(a.ablate) & 16)) gacc_row<S>(L.gacc + 1 * 1024, L.flush, dap, Et, lane, wave, tid);
+        }
         F pad[Tr<S>::KS];
         cl_to_pa<S>(wscr, dap, lane, pad, RND_G(a));
         if (head) {
@@ -1884,10 +2079,10 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
       GE = load_cl(a.GEfin + ro, c, h);
     }
     if (head) {
-      const f32x16 Iv = load_cl(a.I + t * fs + ro, c, h);
+      const f32x16 Iv = ldIh(a, t, ro, c, h);      // kappa I + gamma as the forward formed it
       const f32x16 cev = load_cl(a.ce + t * fs + ro, c, h);
       const f32x16 egv = load_cl(a.eg + t * fs + ro, c, h);
-      const f32x16 Eo = t > 0 ? load_cl(a.E + (t - 1) * fs + ro, c, h) : zero16();
+      const f32x16 Eo = t > 0 ? ldE(a, t - 1, ro, c, h) : zero16();   // full: eh - E_{t-1}
       f32x16 dIl, dEn, dEp, dcE;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -1915,6 +2110,22 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
       store_cl(a.dEp + ro, c, h, rb16(RND_T(a), dEp));
       store_cl(a.dcE + ro, c, h, rb16(RND_T(a), dcE));
     }
+    if constexpr (BF) {
+      if (att_wg) {
+        __syncthreads();                  // the set's 4 rows are staged
+        pr_wgrad_acc<S, PWA_NPX>(st_dap, gi == 0 ? st_xv : st_E, mt, wacc, lane);
+        __syncthreads();                  // before the next set restages
+      }
+    }
+  }
+  float wold[2][4];
+  float* sp = slab_p + gi * 1024 + (16 * mt + 4 * (lane >> 4)) * 32 + (lane & 15);
+  if constexpr (BF) {
+    if (att_wg && !(PT_ABL(a.ablate) & 32))    // the gate tiles' old slab values
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wold[nt][i] = sp[i * 32 + 16 * nt];
   }
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
@@ -1925,7 +2136,15 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   if (bn) bv = bn_bwd_partial(bs0, bs1, L.red, bo, lane, wave, tid);
   PT_TR(a, PT_K_PW_BA, 4);
   if (!(PT_ABL(a.ablate) & 32)) flush_small<9>(sm, slots, L.small, L.slabl, slab_p, lane, wave, tid);   // ends with a barrier
-  if (tail && (head || HG) && !(PT_ABL(a.ablate) & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
+  if constexpr (BF) {
+    if (att_wg && !(PT_ABL(a.ablate) & 32))
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sp[i * 32 + 16 * nt] = wold[nt][i] + wacc[nt][i];
+  } else {
+    if (tail && (head || HG) && !(PT_ABL(a.ablate) & 32)) gacc_flush(L.gacc, L.slabl, slab_p, 0, 2, tid);
+  }
   PT_TR(a, PT_K_PW_BA, 5);
   // L.stat is unused by the backward kernels: mode 2's ticket flag word
   if (bn) bn_publish_finish<PW_NT, false>(bo, blockIdx.x, bv, tid, (int*)L.stat, (double*)L.red);
@@ -1974,11 +2193,11 @@ __device__ __forceinline__ void pw_bb_body(const CellArgs<S>& a, char* smem, int
     w.Iprev = zero16();
     if constexpr (HG) {
       w.ginh = load_cl(a.at + t * fs + ro, c, h);
-      if (t > 0) w.Iprev = load_cl(a.I + (t - 1) * fs + ro, c, h);
+      if (t > 0) w.Iprev = ldI(a, t - 1, ro, c, h);
     } else {
       if (t == 0) w.ginh = zero16();
-      else if (a.no_inh) w.ginh = load_cl(a.E + (t - 1) * fs + ro, c, h);
-      else w.ginh = load_cl(a.I + (t - 1) * fs + ro, c, h);
+      else if (a.no_inh) w.ginh = ldE(a, t - 1, ro, c, h);
+      else w.ginh = ldI(a, t - 1, ro, c, h);
     }
     w.dep = load_pk(a.dEp + ro, c, h);
     w.gEv = load_pk(a.gE + t * fs + ro, c, h);
@@ -2225,11 +2444,11 @@ __device__ __forceinline__ Pb2In<S> pb2_load(const CellArgs<S>& a, int t, size_t
   w.Iprev = zero8();
   if constexpr (HG) {
     w.ginh = pr_load<S>(a.at + t * fs + ro, lane);                    // g_inh = att_t
-    if (t > 0) w.Iprev = pr_load<float>(a.I + (t - 1) * fs + ro, lane);
+    if (t > 0) w.Iprev = prI(a, t - 1, ro, lane);
   } else {
     if (t == 0) w.ginh = zero8();
-    else if (a.no_inh) w.ginh = pr_load<float>(a.E + (t - 1) * fs + ro, lane);
-    else w.ginh = pr_load<float>(a.I + (t - 1) * fs + ro, lane);
+    else if (a.no_inh) w.ginh = prE(a, t - 1, ro, lane);
+    else w.ginh = prI(a, t - 1, ro, lane);
   }
   w.dep = pr_load_pk<S>(a.dEp + ro, lane);
   w.gE = pr_load_pk<S>(a.gE + t * fs + ro, lane);
@@ -2543,17 +2762,17 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_ba2(CellArgs<S> a) {
     if (att_bwd) {
       if (head) {
         w.dgE = pr_load_pk<S>(dgsrc + ro, ln);
-        w.Et = pr_load<float>(a.E + t * fs + ro, ln);
+        w.Et = prEh(a, t, ro, ln);
       }
       if constexpr (HG) w.dAt = pr_load_pk<S>(a.dAt + ro, ln);
     }
     w.Iv = zero8(); w.Eo = zero8();
     w.ce = PrPk<S>{}; w.eg = PrPk<S>{}; w.dEn = PrPk<S>{};
     if (head) {
-      w.Iv = pr_load<float>(a.I + t * fs + ro, ln);
+      w.Iv = prIh(a, t, ro, ln);
       w.ce = pr_load_pk<S>(a.ce + t * fs + ro, ln);
       w.eg = pr_load_pk<S>(a.eg + t * fs + ro, ln);
-      if (t > 0) w.Eo = pr_load<float>(a.E + (t - 1) * fs + ro, ln);
+      if (t > 0) w.Eo = prE(a, t - 1, ro, ln);
       if (tail) w.dEn = pr_load_pk<S>(a.dEn + ro, ln);
     }
     return w;
@@ -3516,6 +3735,27 @@ __global__ __launch_bounds__(256) void k_to_nchw(const S* __restrict__ src, floa
     if (c < Cu) dst[nchw_off(v, y * IMG + px, c, T, t, ntx, nty, Cu)] = tl[px][c];
   }
 }
+// The same for a state (E) of the bf16 cell: f32 restored from its hi / lo
+// planes (CellArgs::Eh / El), a channel pair per 4-B load of each plane.
+__global__ __launch_bounds__(256) void k_split_to_nchw(const uint16_t* __restrict__ hi,
+                                                       const uint16_t* __restrict__ lo, float* __restrict__ dst,
+                                                       int B, int T, int t, int ntx, int nty, int Cu) {
+  __shared__ float tl[IMG][C + 1];
+  const int v = blockIdx.x / IMG, y = blockIdx.x % IMG;
+  const size_t o = ((size_t)v * NPIX + (size_t)y * IMG) * C;
+  const uint32_t* wh = (const uint32_t*)(hi + o);
+  const uint32_t* wl = (const uint32_t*)(lo + o);
+  for (int i = threadIdx.x; i < IMG * C / 2; i += 256) {
+    const uint32_t x = wh[i], w = wl[i];
+    tl[(2 * i) / C][(2 * i) % C] = __uint_as_float((x << 16) + (uint32_t)((int32_t)(w << 16) >> 16));
+    tl[(2 * i) / C][(2 * i) % C + 1] = __uint_as_float((x & 0xffff0000u) + (uint32_t)((int32_t)w >> 16));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < IMG * C; i += 256) {
+    const int c = i / IMG, px = i % IMG;
+    if (c < Cu) dst[nchw_off(v, y * IMG + px, c, T, t, ntx, nty, Cu)] = tl[px][c];
+  }
+}
 __global__ __launch_bounds__(256) void k_from_nchw(const float* __restrict__ src, float* __restrict__ dst,
                                                    int B, int ntx, int nty, int Cu) {
   __shared__ float tl[IMG][C + 1];
@@ -3730,6 +3970,8 @@ int check(const pt_cell_desc* d) {
   return 0;
 }
 
+inline size_t fbytes_of(const Plan& p) { return al(p.frame * p.T * p.es); }
+
 Plan plan(const pt_cell_desc* d) {
   Plan p{};
   p.ntx = d->width / IMG; p.nty = d->height / IMG;
@@ -3738,14 +3980,16 @@ Plan plan(const pt_cell_desc* d) {
   p.frame = (size_t)p.B * NPIX * C;
   const size_t fbytes = al(p.frame * p.T * p.es);
   size_t o = 0;
-  p.o_E = o; o += al(p.frame * p.T * 4);          // f32 in both modes (CellArgs::E)
-  p.o_I = o; o += al(p.frame * p.T * 4);          // f32 in both modes (CellArgs::I)
+  // E, I: f32 cell: f32 arrays; bf16 cell: hi plane then lo plane (CellArgs::Eh /
+  // El, Ic / Il), the same 4 bytes per element, and I's hi plane is Ic
+  p.o_E = o; o += p.es == 2 ? 2 * fbytes : al(p.frame * p.T * 4);
+  p.o_I = o; o += p.es == 2 ? 2 * fbytes : al(p.frame * p.T * 4);
   p.o_gE = o; o += fbytes;
   p.o_ci = o; o += fbytes;
   p.o_ce = o; o += fbytes;
   p.o_eg = o; o += fbytes;
   p.o_at = o; o += d->cell == PT_CELL_HGRU ? fbytes : 0;
-  p.o_Ic = o; o += p.es == 2 ? fbytes : 0;         // bf16 copy of I (f32: I itself)
+  p.o_Ic = p.o_I;                                 // bf16: I's hi plane; f32: I itself
   p.o_bnstat = o; o += al((size_t)p.T * 128 * 4);
   for (int i = 0; i < 4; ++i) { p.o_wf[i] = o; o += al((size_t)C * C * p.K * p.K * p.es); }
   for (int i = 0; i < 12; ++i) { p.o_g[i] = o; o += al((size_t)C * C * p.es); }
@@ -3805,8 +4049,16 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
     a.g16f[i] = (const typename CellArgs<S>::F16*)(saved + p.o_g16[i]);
     a.g16t[i] = (const typename CellArgs<S>::F16*)(saved + p.o_g16[6 + i]);
   }
-  a.E = (float*)(saved + p.o_E); a.I = (float*)(saved + p.o_I);
-  a.Ic = p.es == 2 ? (S*)(saved + p.o_Ic) : (S*)(saved + p.o_I); a.gE = (S*)(saved + p.o_gE);
+  if (p.es == 2) {            // bf16: split planes (CellArgs::Eh); no f32 arrays
+    a.E = nullptr; a.I = nullptr;
+    a.Eh = (S*)(saved + p.o_E); a.El = (uint16_t*)(saved + p.o_E + fbytes_of(p));
+    a.Ic = (S*)(saved + p.o_I); a.Il = (uint16_t*)(saved + p.o_I + fbytes_of(p));
+  } else {
+    a.E = (float*)(saved + p.o_E); a.I = (float*)(saved + p.o_I);
+    a.Eh = nullptr; a.El = nullptr; a.Il = nullptr;
+    a.Ic = (S*)(saved + p.o_I);
+  }
+  a.gE = (S*)(saved + p.o_gE);
   a.ci = (S*)(saved + p.o_ci); a.ce = (S*)(saved + p.o_ce); a.eg = (S*)(saved + p.o_eg);
   a.at = a.hgru ? (S*)(saved + p.o_at) : nullptr;
   a.bnstat = (float*)(saved + p.o_bnstat);
@@ -3871,19 +4123,19 @@ int set_lds_attrs() {
   SETLDS((k_bnbwd_fill<S>), conv_lds_bytes<S>());
   SETLDS((k_pw_fa<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_ba<S, 0, 0>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_ba<S, 0, 0>), (pwa_lds_bytes<S>()));
   SETLDS((k_pw_bb<S, 0, 0>), (pwb_lds_bytes<S>()));
   SETLDS((k_pw_fa<S, 0, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 1>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_ba<S, 0, 1>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_ba<S, 0, 1>), (pwa_lds_bytes<S>()));
   SETLDS((k_pw_bb<S, 0, 1>), (pwb_lds_bytes<S>()));
   SETLDS((k_pw_fa<S, 1, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 1, 0>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_ba<S, 1, 0>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_ba<S, 1, 0>), (pwa_lds_bytes<S>()));
   SETLDS((k_pw_bb<S, 1, 0>), (pwb_lds_bytes<S>()));
   SETLDS((k_pw_fa<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 1, 1>), (pw_lds_bytes<PWF_RPP, false>()));
-  SETLDS((k_pw_ba<S, 1, 1>), (pw_lds_bytes<PWA_RPP, true>()));
+  SETLDS((k_pw_ba<S, 1, 1>), (pwa_lds_bytes<S>()));
   SETLDS((k_pw_bb<S, 1, 1>), (pwb_lds_bytes<S>()));
   SETLDS((k_pw_bb2<S, 0, 0>), (pb2_lds_bytes<S>()));
   SETLDS((k_pw_bb2<S, 0, 1>), (pb2_lds_bytes<S>()));
@@ -4117,10 +4369,15 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
     if (syncbn(dist))
       if (int rc = bn_sync(dist, cb.bnout.grp, bn_ngrp(p.B), 96, ((size_t)t * 2 + 1) * 96, st)) return rc;
   }
-  if (e_last)
-    hipLaunchKernelGGL(k_to_nchw<float>, dim3(p.B * IMG), dim3(256), 0, st,
-                       (const float*)a.E + (size_t)(p.T - 1) * p.frame, e_last, p.B, 1, 0, p.ntx, p.nty,
-                       p.Cu);
+  if (e_last) {
+    const size_t o = (size_t)(p.T - 1) * p.frame;
+    if (p.es == 2)
+      hipLaunchKernelGGL(k_split_to_nchw, dim3(p.B * IMG), dim3(256), 0, st, (const uint16_t*)a.Eh + o,
+                         (const uint16_t*)a.El + o, e_last, p.B, 1, 0, p.ntx, p.nty, p.Cu);
+    else
+      hipLaunchKernelGGL(k_to_nchw<float>, dim3(p.B * IMG), dim3(256), 0, st, (const float*)a.E + o, e_last,
+                         p.B, 1, 0, p.ntx, p.nty, p.Cu);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -4187,7 +4444,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   hipLaunchKernelGGL(k_from_nchw, dim3(p.B * IMG), dim3(256), 0, st, d_e_last,
                      (float*)((char*)ws + p.o_tr[NTRANS - 1]), p.B, p.ntx, p.nty, p.Cu);
   const dim3 gpa(p.B * PWA_WGPC), gpb(p.B * PWB_WGPC);
-  const size_t lpa = (pw_lds_bytes<PWA_RPP, true>()), lpb = pwb_lds_bytes<S>();
+  const size_t lpa = pwa_lds_bytes<S>(), lpb = pwb_lds_bytes<S>();
   const size_t lcv = conv_lds_bytes<S>();
   const size_t fs = p.frame;
   const float* bst = a.bnstat;
@@ -4334,9 +4591,16 @@ int pt_cell_export_exc(const pt_cell_desc* d, const void* saved, float* e_seq, p
   if (!saved || !e_seq) return fail(PT_ERR_ARG, "null pointer argument%s%ld");
   const Plan p = plan(d);
   for (int t = 0; t < p.T; ++t) {
-    hipLaunchKernelGGL(k_to_nchw<float>, dim3(p.B * IMG), dim3(256), 0, (hipStream_t)stream,   // E is f32
-                       (const float*)((const char*)saved + p.o_E) + (size_t)t * p.frame, e_seq, p.B,
-                       p.T, t, p.ntx, p.nty, p.Cu);
+    const size_t o = (size_t)t * p.frame;
+    if (p.es == 2) {          // E_t restored exactly from its planes (CellArgs::Eh)
+      const uint16_t* hi = (const uint16_t*)((const char*)saved + p.o_E);
+      const uint16_t* lo = (const uint16_t*)((const char*)saved + p.o_E + fbytes_of(p));
+      hipLaunchKernelGGL(k_split_to_nchw, dim3(p.B * IMG), dim3(256), 0, (hipStream_t)stream, hi + o, lo + o,
+                         e_seq, p.B, p.T, t, p.ntx, p.nty, p.Cu);
+    } else {
+      hipLaunchKernelGGL(k_to_nchw<float>, dim3(p.B * IMG), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)((const char*)saved + p.o_E) + o, e_seq, p.B, p.T, t, p.ntx, p.nty, p.Cu);
+    }
   }
   HIPCHK(hipGetLastError());
   return 0;

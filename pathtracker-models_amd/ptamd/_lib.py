@@ -97,15 +97,16 @@ class diag_library:
 
     def __enter__(self):
         global _override
-        _lock.acquire()
-        self._prev = _override
-        _override = DIAG_PATH
-        return _open(DIAG_PATH)
+        lib = _open(DIAG_PATH)
+        with _lock:           # not held across the block: autograd's backward thread loads too
+            self._prev = _override
+            _override = DIAG_PATH
+        return lib
 
     def __exit__(self, *exc):
         global _override
-        _override = self._prev
-        _lock.release()
+        with _lock:
+            _override = self._prev
         return False
 
 

@@ -173,6 +173,7 @@ class RecurrentCellFn(torch.autograd.Function):
             _lib.check(lib.pt_cell_export_exc(ctypes.byref(d), _ptr(saved), _ptr(e_seq), st))
         ctx.cfg = cfg
         ctx.cdist = cdist
+        ctx.lib = lib                      # the backward runs on the library that wrote `saved`
         ctx.saved_blob = saved
         ctx.save_for_backward(x, *[p if p is not None else torch.empty(0) for p in params])
         ctx.has = [p is not None for p in params]
@@ -181,7 +182,7 @@ class RecurrentCellFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, d_e_last, _d_seq, _d_gates):
-        lib = _lib.load()
+        lib = ctx.lib
         x, *params = ctx.saved_tensors
         params = [p if has else None for p, has in zip(params, ctx.has)]
         c = params[0].shape[0]
