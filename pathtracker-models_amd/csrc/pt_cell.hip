@@ -566,15 +566,20 @@ __device__ __forceinline__ f32x16 load_cl_split(const bf16_t* __restrict__ hi, c
   }
   return v;
 }
-__device__ __forceinline__ void store_cl_split(bf16_t* __restrict__ hi, uint16_t* __restrict__ lo, int c, int h,
-                                               const f32x16& v) {
+// stores the split and returns the hi plane's values (the bf16 operand value,
+// so a caller that also needs it does not round a second time)
+__device__ __forceinline__ f32x16 store_cl_split(bf16_t* __restrict__ hi, uint16_t* __restrict__ lo, int c, int h,
+                                                 const f32x16& v) {
   uint16_t* hp = (uint16_t*)hi;
+  f32x16 hv;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const uint32_t b = __float_as_uint(v[r]), hh = (b + 0x8000u) >> 16;
-    hp[cl_x(r, h) * C + c] = (uint16_t)hh;
-    lo[cl_x(r, h) * C + c] = (uint16_t)(b - (hh << 16));
+    const uint32_t b = __float_as_uint(v[r]), hh = (b + 0x8000u) & 0xffff0000u;
+    hp[cl_x(r, h) * C + c] = (uint16_t)(hh >> 16);
+    lo[cl_x(r, h) * C + c] = (uint16_t)(b - hh);
+    hv[r] = __uint_as_float(hh);
   }
+  return hv;
 }
 // PR (pt_pr.h) half-row tile of a split state: the lane's channel pair is one
 // dword per plane
@@ -618,17 +623,26 @@ __device__ __forceinline__ f32x16 ldIh(const CellArgs<S>& a, int t, size_t ro, i
   if constexpr (sizeof(S) == 2) return load_cl(a.Ic + o, c, h);
   else return load_cl(a.I + o, c, h);
 }
+// (both return op_round<S>(v): the value the bf16 operands take)
 template <class S>
-__device__ __forceinline__ void stE(const CellArgs<S>& a, int t, size_t ro, int c, int h, const f32x16& v) {
+__device__ __forceinline__ f32x16 stE(const CellArgs<S>& a, int t, size_t ro, int c, int h, const f32x16& v) {
   const size_t o = fr_off(t, a.B) + ro;
-  if constexpr (sizeof(S) == 2) store_cl_split(a.Eh + o, a.El + o, c, h, v);
-  else store_cl(a.E + o, c, h, v);
+  if constexpr (sizeof(S) == 2) {
+    return store_cl_split(a.Eh + o, a.El + o, c, h, v);
+  } else {
+    store_cl(a.E + o, c, h, v);
+    return v;
+  }
 }
 template <class S>
-__device__ __forceinline__ void stI(const CellArgs<S>& a, int t, size_t ro, int c, int h, const f32x16& v) {
+__device__ __forceinline__ f32x16 stI(const CellArgs<S>& a, int t, size_t ro, int c, int h, const f32x16& v) {
   const size_t o = fr_off(t, a.B) + ro;
-  if constexpr (sizeof(S) == 2) store_cl_split(a.Ic + o, a.Il + o, c, h, v);
-  else store_cl(a.I + o, c, h, v);
+  if constexpr (sizeof(S) == 2) {
+    return store_cl_split(a.Ic + o, a.Il + o, c, h, v);
+  } else {
+    store_cl(a.I + o, c, h, v);
+    return v;
+  }
 }
 template <class S>
 __device__ __forceinline__ f32x8 prE(const CellArgs<S>& a, int t, size_t ro, int lane) {
@@ -1603,7 +1617,7 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
   const float nba = sig_nb(a.gb[0][c] + a.gb[1][c]), nbe = sig_nb(a.gb[4][c] + a.gb[5][c]);
 
   // close frame t-1 (:172-175)
-  f32x16 Ep = zero16();
+  f32x16 Ep = zero16(), Eop = zero16();   // Eop: E_{t-1} as the gates' bf16 operand (= its hi plane)
   if (t > 0) {
     const float A1 = bw1 * rs1, B1 = bb1 - bw1 * rs1 * m1;     // BN1 affine folded
 #pragma unroll
@@ -1616,10 +1630,9 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
     if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 2048))
 #pragma unroll
       for (int r = 0; r < 16; ++r) Ep[r] = (float)(bf16_t)Ep[r];
-    stE(a, t - 1, ro, c, h, Ep);
+    Eop = stE(a, t - 1, ro, c, h, Ep);
   }
   if (t == T) return;
-  const f32x16 Eop = op_round<S>(Ep);      // E_{t-1} as the gates' bf16 operand (= its hi plane)
   f32x16 z, xv;
   stem_cl<ACT>(xs, yl, h, st, z, xv);
   F pax[Tr<S>::KS], pae[Tr<S>::KS];
@@ -1749,8 +1762,8 @@ __device__ __forceinline__ void fb_row(const CellArgs<S>& a, int t, const float*
   if (sizeof(S) == 4 && (PT_ABL(a.ablate) & 4096))
 #pragma unroll
     for (int r = 0; r < 16; ++r) In[r] = (float)(bf16_t)In[r];
-  stI(a, t, ro, c, h, In);                 // bf16: the hi plane is Ic, the exc conv's input
-  if (tile) tile_put_cl(tile, y, c, h, op_round<S>(In));
+  const f32x16 Ih = stI(a, t, ro, c, h, In);   // bf16: the hi plane is Ic, the exc conv's input
+  if (tile) tile_put_cl(tile, y, c, h, Ih);
 }
 
 template <class S, int ACT, int HG>
