@@ -102,26 +102,30 @@ def algorithmic_bytes(kind, batch, frames, elt, xb=4, fused=False):
     """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
     (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
     XF = one clip-frame of the input (3x32x32; xb = 4 B f32, 1 B raw u8 clips).
-    The excitation E and (r04) the inhibition I are f32 in both cell dtypes
-    (DESIGN.md §4): each E or I tile a kernel moves counts F + dE bytes (dE:
-    the extra 2 B per element in bf16); k_fused_fb / k_pw_fb also write the
-    storage-type copy Ic of I_t (the exc conv's input, k_wgrad's X).
-    Implementation overhead (the per-workgroup gradient partials, BatchNorm
-    sums) is not algorithmic and is not counted."""
+    The excitation E and the inhibition I keep their f32 values in both cell
+    dtypes: a full-precision E or I tile counts F + dE bytes
+    (dE: the extra 2 B per element in bf16: the f32 array, or (r05) the hi +
+    lo planes), a read of only its bf16 operand value F (the hi plane; I's
+    hi plane is the exc conv's input and k_wgrad's X).  Implementation
+    overhead (the per-workgroup gradient partials, BatchNorm sums) is not
+    algorithmic and is not counted."""
     F, XF = C * HW * HW * elt, 3 * HW * HW * xb
     dE = C * HW * HW * (4 - elt)
     if fused:       # the conv reads its input from the LDS tile the point-wise half wrote
-        fwd = {"k_fused_fa": frames * (XF + 7 * F + 3 * dE + F),
-               "k_fused_fb": frames * (XF + 3 * F + 2 * dE + 2 * F),
-               "k_pw_fa": 3 * F + 3 * dE + 2 * F}        # closes E_{T-1} only
+        # fa: E_{t-2} full, I_{t-1} hi, eg, ce in; E_{t-1} full, gE, eg, ci out
+        # fb: c_i, I_{t-1} full in; I_t full, c_e out
+        fwd = {"k_fused_fa": frames * (XF + 8 * F + 2 * dE),
+               "k_fused_fb": frames * (XF + 4 * F + 2 * dE),
+               "k_pw_fa": 5 * F + 2 * dE}                # closes E_{T-1} only
         if kind in fwd or kind in ("k_pw_fb", "k_conv_fa", "k_conv_fb"):
             return fwd.get(kind, 0) * batch
     per_clip = {
-        "k_pw_fa": frames * (XF + 7 * F + 3 * dE),
+        "k_pw_fa": frames * (XF + 7 * F + 2 * dE),
         "k_conv_fa": frames * 2 * F,
         "k_pw_fb": frames * (XF + 4 * F + 2 * dE),
         "k_conv_fb": frames * 2 * F,
-        "k_pw_ba": frames * (XF + 11 * F + 3 * dE),
+        # dgE, E_t hi, dEn, I_t hi, ce, eg, E_{t-1} full in; dIl, dEn, dEp, dcE out
+        "k_pw_ba": frames * (XF + 11 * F + dE),
         "k_conv_ba": (frames - 1) * 5 * F + 3 * F,
         "k_pw_bb": frames * (XF + 8 * F + dE),
         "k_conv_bb": frames * 6 * F,

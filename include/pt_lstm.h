@@ -117,6 +117,26 @@ int pt_lstm_stem_backward(const void* x, int x_u8, const float* w, const float* 
                           int B, int cin, int cout, long long n, void* workspace, float* dw,
                           float* db, pt_lstm_stream_t stream);
 
+/* The clip ConvLSTM with its frame stem fused in: desc.x_seq
+ * must be 1, desc.init_state 0, desc.in_channels = the stem's outputs.  x is
+ * the raw clip batch the stem takes (f32 [B,cin_s,T,H,W], or x_u8 = 1: u8
+ * [B,T,H,W,cin_s]; cin_s 1..4) and the recurrence's per-step input is
+ * softplus(ws x + bs) (ws [in_channels,cin_s], bs [in_channels]), computed
+ * exactly as pt_lstm_stem_forward does but written straight into the
+ * recurrence's own buffer: the f32 [B,in_channels,T,H,W] stem output and its
+ * layout conversion never exist.  The backward does pt_lstm_backward's work
+ * and then the stem's dW (dws [in_channels,cin_s]) and db (dbs) straight from
+ * the recurrence's d x_t (either may be NULL); g->d_x may be NULL.
+ * Replaces pt_lstm_stem_forward + pt_lstm_forward (and the backward pair) for
+ * models/convlstm.py's ConvLSTMVideo. */
+int pt_lstm_forward_stem(const pt_lstm_desc* d, const void* x, int x_u8, int cin_s, const float* ws,
+                         const float* bs, const pt_lstm_params* p, void* saved, float* h_out,
+                         float* c_out, pt_lstm_stream_t stream);
+int pt_lstm_backward_stem(const pt_lstm_desc* d, const void* x, int x_u8, int cin_s, const float* ws,
+                          const float* bs, const void* saved, void* workspace, const float* d_h,
+                          const float* d_c, const pt_lstm_grads* g, float* dws, float* dbs,
+                          pt_lstm_stream_t stream);
+
 const char* pt_lstm_last_error(void);
 const char* pt_lstm_version(void);
 

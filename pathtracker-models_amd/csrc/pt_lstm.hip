@@ -1081,6 +1081,119 @@ __global__ __launch_bounds__(256) void k_stem_bwd(const void* __restrict__ x, in
     part[(size_t)blockIdx.x * NA + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
+// The clip ConvLSTM's stem fused into the recurrence (pt_lstm_forward_stem):
+// y = softplus(W x + b) of 4 voxels per thread, computed exactly as k_stem_fwd
+// does, stored straight into the recurrence's per-step input, channels-last
+// [T][B][NPIX][32] in S with the channels >= cout zero -- bit for bit what
+// k_to_cl_seq makes of k_stem_fwd's f32 [B][cout][T][NPIX], which therefore
+// never exists.  One workgroup per (frame t, clip b) image, [T][B] order.
+template <int CIN, class S>
+__global__ __launch_bounds__(256) void k_stem_cl_fwd(const void* __restrict__ x, int xu8, const float* __restrict__ w,
+                                                     const float* __restrict__ b, S* __restrict__ dst, int cout,
+                                                     int B, int T) {
+  const int img = blockIdx.x, t = img / B, bi = img - t * B, tid = threadIdx.x;
+  const long n4 = (long)T * (NPIX / 4), v = (long)t * (NPIX / 4) + tid;   // pixels 4 tid .. 4 tid + 3
+  float4 xi[CIN];
+  stem_load<CIN>(x, xu8, bi, v, n4, xi);
+  S* d = dst + ((size_t)img * NPIX + 4 * tid) * HC;
+  constexpr int CPB = 16 / (int)sizeof(S);
+#pragma unroll
+  for (int q = 0; q < HC / CPB; ++q) {
+    float yv[4][CPB];
+#pragma unroll
+    for (int j = 0; j < CPB; ++j) {
+      const int o = q * CPB + j;
+      float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (o < cout) {
+        float4 z = make_float4(b[o], b[o], b[o], b[o]);
+#pragma unroll
+        for (int k = 0; k < CIN; ++k) {
+          const float wk = w[o * CIN + k];
+          z.x += wk * xi[k].x; z.y += wk * xi[k].y; z.z += wk * xi[k].z; z.w += wk * xi[k].w;
+        }
+        y = make_float4(softplus20(z.x), softplus20(z.y), softplus20(z.z), softplus20(z.w));
+      }
+      yv[0][j] = y.x; yv[1][j] = y.y; yv[2][j] = y.z; yv[3][j] = y.w;
+    }
+#pragma unroll
+    for (int vx = 0; vx < 4; ++vx) {
+      if constexpr (sizeof(S) == 2) {
+        u32x4 o4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+          const bf2 pr = {(S)yv[vx][2 * j], (S)yv[vx][2 * j + 1]};
+          o4[j] = __builtin_bit_cast(uint32_t, pr);
+        }
+        *(u32x4*)(d + vx * HC + q * CPB) = o4;
+      } else {
+        *(f32x4*)(d + vx * HC + q * CPB) = f32x4{yv[vx][0], yv[vx][1], yv[vx][2], yv[vx][3]};
+      }
+    }
+  }
+}
+
+// dW [cout][CIN], db [cout] of the fused stem from the recurrence's d x_t of
+// all steps, channels-last f32 [T][B][NPIX][32] (the all-steps transposed
+// conv's output), so the f32 [B][cout][T][NPIX] gradient tensor never exists
+// either.  One thread per voxel: its 32 channels of d x_t are 128 contiguous
+// bytes (8 x 16-B loads, a wave reads 8 KB in one run); z recomputed from x
+// as k_stem_bwd does; per-block partials summed by k_stem_reduce.
+template <int CIN>
+__global__ __launch_bounds__(256) void k_stem_cl_bwd(const void* __restrict__ x, int xu8, const float* __restrict__ w,
+                                                     const float* __restrict__ b, const float* __restrict__ dxs,
+                                                     float* __restrict__ part, int cout, int B, int T) {
+  constexpr int NA = 32 * (CIN + 1);
+  float acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = 0.f;
+  const long n = (long)T * NPIX, total = (long)B * n;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    // voxel e in [T][B][NPIX] order (the d x_t layout): frame t, clip bi, pixel p
+    const long t = e / ((long)B * NPIX), r = e - t * B * NPIX, bi = r / NPIX, p = r - bi * NPIX;
+    const long vox = t * NPIX + p;                     // within clip bi
+    float xi[CIN];
+    if (xu8) {
+      const uint8_t* q = (const uint8_t*)x + (bi * n + vox) * CIN;
+#pragma unroll
+      for (int k = 0; k < CIN; ++k) xi[k] = (float)((double)q[k] / 255.0);
+    } else {
+#pragma unroll
+      for (int k = 0; k < CIN; ++k) xi[k] = ((const float*)x)[(bi * CIN + k) * n + vox];
+    }
+    const f32x4* dp = (const f32x4*)(dxs + (size_t)e * HC);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const f32x4 d4 = dp[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = 4 * q + j;
+        if (o < cout) {
+          float z = b[o];
+#pragma unroll
+          for (int k = 0; k < CIN; ++k) z += w[o * CIN + k] * xi[k];
+          const float gz = dsoftplus20(z, d4[j]);
+#pragma unroll
+          for (int k = 0; k < CIN; ++k) acc[o * (CIN + 1) + k] += gz * xi[k];
+          acc[o * (CIN + 1) + CIN] += gz;
+        }
+      }
+    }
+  }
+  __shared__ float red[4][NA];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    float t = acc[i];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+    if (lane == 0) red[wv][i] = t;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NA; i += blockDim.x)
+    part[(size_t)blockIdx.x * NA + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
 // One workgroup per accumulator: 256 threads stride the partials, then a
 // fixed-order tree in LDS (deterministic), fp64 throughout.
 __global__ __launch_bounds__(256) void k_stem_reduce(const float* __restrict__ part, int nblk, int cin,
@@ -1121,6 +1234,11 @@ namespace {
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
+constexpr int STEM_BLOCKS = 1024;     // stem weight-gradient partials (k_stem_bwd / k_stem_cl_bwd)
+// pt_lstm_forward_stem / pt_lstm_backward_stem: the raw clip batch and the
+// stem's parameters (the recurrence's input channels = the stem's outputs)
+struct StemIn { const void* x; int xu8, cin; const float *w, *b; };
+
 struct LPlan {
   int B, T, K, ch, cin, nsl_h, nsl_x, nb;
   int xseq;           // one input image per step (desc.x_seq)
@@ -1128,7 +1246,7 @@ struct LPlan {
   // saved
   size_t o_fr[4], o_bias, o_x, o_xg, o_h0, o_c0, o_P, o_h, o_c, saved;
   // workspace
-  size_t o_dh, o_dc, o_dP, o_dPsum, o_dPsumS, o_jvP, o_wsh, o_wsx, o_col, o_dx, ws;
+  size_t o_dh, o_dc, o_dP, o_dPsum, o_dPsumS, o_jvP, o_wsh, o_wsx, o_col, o_dx, o_stem, ws;
 };
 
 int check(const pt_lstm_desc* d) {
@@ -1191,6 +1309,8 @@ LPlan plan(const pt_lstm_desc* d) {
   p.o_col = o; o += al((size_t)p.nb * GC * 4);
   // per-step input: d x_t of all steps from ONE transposed conv over B*T images
   p.o_dx = o; o += p.xseq ? al(p.npix * HC * 4 * p.T) : 0;
+  // the fused stem's per-block partials (pt_lstm_backward_stem, up to 4 input channels)
+  p.o_stem = o; o += p.xseq ? al((size_t)STEM_BLOCKS * 32 * 5 * 4) : 0;
   p.ws = o;
   return p;
 }
@@ -1312,7 +1432,8 @@ inline dim3 grid_for(size_t n, int bs = 256) {
 
 template <class S>
 int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr, const float* h0,
-                const float* c0, char* sv, float* h_out, float* c_out, hipStream_t st) {
+                const float* c0, char* sv, float* h_out, float* c_out, hipStream_t st,
+                const StemIn* sm = nullptr) {
   const LPlan p = plan(d);
   const int npix = (int)p.npix;
   LPrepArgs pa{};
@@ -1327,7 +1448,13 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   HIPCHK(hipGetLastError());
 
   S* xcl = (S*)(sv + p.o_x);
-  if (p.xseq)
+  if (sm) {                  // the stem straight into the per-step input (k_stem_cl_fwd)
+    switch (sm->cin) {
+#define STEM_CF(CI) case CI: hipLaunchKernelGGL((k_stem_cl_fwd<CI, S>), dim3(p.B * p.T), dim3(256), 0, st, sm->x, sm->xu8, sm->w, sm->b, xcl, p.cin, p.B, p.T); break;
+      STEM_CF(1) STEM_CF(2) STEM_CF(3) STEM_CF(4)
+#undef STEM_CF
+    }
+  } else if (p.xseq)
     hipLaunchKernelGGL(k_to_cl_seq<S>, dim3(p.B * p.T * (NPIX / SEQ_CH)), dim3(256), 0, st, x, xcl,
                        p.B, p.cin, p.T);
   else
@@ -1375,7 +1502,8 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
 template <class S>
 int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
                  const float* d_h, const float* d_c, const pt_lstm_grads* g, int has_h0,
-                 int has_c0, hipStream_t st) {
+                 int has_c0, hipStream_t st, const StemIn* sm = nullptr, float* dws = nullptr,
+                 float* dbs = nullptr) {
   const LPlan p = plan(d);
   const int npix = (int)p.npix;
   const size_t pstep = p.npix * GC, hstep = p.npix * HC;
@@ -1440,13 +1568,26 @@ int run_backward(const pt_lstm_desc* d, const char* sv, char* ws,
   for (int i = 0; i < 4; ++i) { ra.wh[i] = g->wh[i]; ra.wx[i] = g->wx[i]; ra.bx[i] = g->bx[i]; }
   hipLaunchKernelGGL(k_lreduce, dim3(1024), dim3(256), 0, st, ra);
   HIPCHK(hipGetLastError());
-  if (g->d_x) {
+  const bool stem_g = sm && (dws || dbs);
+  if (g->d_x || stem_g) {
     if (p.xseq) {        // all steps' d x_t from one transposed conv over the B*T images
       float* dxs = (float*)(ws + p.o_dx);
       if (int rc = conv_k<S, 4, 1>(p.K, dP, sv + p.o_fr[3], dxs, nullptr, nullptr, p.B * p.T, st))
         return rc;
-      hipLaunchKernelGGL(k_from_cl_seq<float>, dim3(p.B * p.T * (NPIX / SEQ_CH)), dim3(256), 0, st,
-                         (const float*)dxs, g->d_x, p.B, p.cin, p.T);
+      if (stem_g) {      // the fused stem's dW / db straight from d x_t (k_stem_cl_bwd)
+        float* part = (float*)(ws + p.o_stem);
+        switch (sm->cin) {
+#define STEM_CB(CI) case CI: hipLaunchKernelGGL(k_stem_cl_bwd<CI>, dim3(STEM_BLOCKS), dim3(256), 0, st, sm->x, sm->xu8, sm->w, sm->b, (const float*)dxs, part, p.cin, p.B, p.T); break;
+          STEM_CB(1) STEM_CB(2) STEM_CB(3) STEM_CB(4)
+#undef STEM_CB
+        }
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_stem_reduce, dim3(32 * (sm->cin + 1)), dim3(256), 0, st, (const float*)part,
+                           STEM_BLOCKS, sm->cin, p.cin, dws, dbs);
+      }
+      if (g->d_x)
+        hipLaunchKernelGGL(k_from_cl_seq<float>, dim3(p.B * p.T * (NPIX / SEQ_CH)), dim3(256), 0, st,
+                           (const float*)dxs, g->d_x, p.B, p.cin, p.T);
     } else {
       if (int rc = conv_k<S, 4, 1>(p.K, dPsumS, sv + p.o_fr[3], dh, nullptr, nullptr, p.B, st))
         return rc;
@@ -1478,7 +1619,6 @@ int run_jv(const pt_lstm_desc* d, const char* sv, char* ws, float mu, float* jv,
   return 0;
 }
 
-constexpr int STEM_BLOCKS = 1024;
 
 int stem_check(const void* x, const float* w, int B, int cin, int cout, long long n) {
   if (!x || !w) return fail(PT_LSTM_ERR_ARG, "null x / w%ld");
@@ -1536,6 +1676,56 @@ int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace, 
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
   k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
+  return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
+}
+
+int pt_lstm_forward_stem(const pt_lstm_desc* d, const void* x, int x_u8, int cin_s, const float* ws,
+                         const float* bs, const pt_lstm_params* p, void* saved, float* h_out,
+                         float* c_out, pt_lstm_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  if (!d->x_seq) return fail(PT_LSTM_ERR_UNSUPPORTED, "the fused stem needs x_seq = 1%ld");
+  if (d->init_state) return fail(PT_LSTM_ERR_UNSUPPORTED, "the fused stem starts from h0 = c0 = 0 (init_state %ld)", d->init_state);
+  if (int rc = stem_check(x, ws, d->batch, cin_s, d->in_channels, 4)) return rc;
+  if (x_u8 != 0 && x_u8 != 1) return fail(PT_LSTM_ERR_ARG, "bad x_u8 (%ld)", x_u8);
+  if (!bs || !p || !saved) return fail(PT_LSTM_ERR_ARG, "null bs / params / saved%ld");
+  const bool bf = d->dtype == PT_LSTM_BF16;
+  if (int rc = bf ? prime<bf16_t>(d->ksize) : prime<float>(d->ksize)) return rc;
+  const StemIn sm{x, x_u8, cin_s, ws, bs};
+  auto body = [&](hipStream_t s) {
+    return bf ? run_forward<bf16_t>(d, nullptr, p, nullptr, nullptr, (char*)saved, h_out, c_out, s, &sm)
+              : run_forward<float>(d, nullptr, p, nullptr, nullptr, (char*)saved, h_out, c_out, s, &sm);
+  };
+  hipStream_t st = (hipStream_t)stream;
+  if (!ptg::graphs_enabled()) return body(st);
+  ptg::Key k;
+  k.add(3).add(*d).add(x).add(x_u8).add(cin_s).add(ws).add(bs).add(*p).add(saved).add(h_out).add(c_out)
+      .add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
+  return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
+}
+
+int pt_lstm_backward_stem(const pt_lstm_desc* d, const void* x, int x_u8, int cin_s, const float* ws,
+                          const float* bs, const void* saved, void* workspace, const float* d_h,
+                          const float* d_c, const pt_lstm_grads* g, float* dws, float* dbs,
+                          pt_lstm_stream_t stream) {
+  if (int rc = check(d)) return rc;
+  if (!d->x_seq || d->init_state)
+    return fail(PT_LSTM_ERR_UNSUPPORTED, "the fused stem needs x_seq = 1 and h0 = c0 = 0 (init_state %ld)", d->init_state);
+  if (int rc = stem_check(x, ws, d->batch, cin_s, d->in_channels, 4)) return rc;
+  if (x_u8 != 0 && x_u8 != 1) return fail(PT_LSTM_ERR_ARG, "bad x_u8 (%ld)", x_u8);
+  if (!bs || !saved || !workspace || !d_h || !g)
+    return fail(PT_LSTM_ERR_ARG, "null bs / saved / workspace / d_h / grads%ld");
+  const bool bf = d->dtype == PT_LSTM_BF16;
+  if (int rc = bf ? prime<bf16_t>(d->ksize) : prime<float>(d->ksize)) return rc;
+  const StemIn sm{x, x_u8, cin_s, ws, bs};
+  auto body = [&](hipStream_t s) {
+    return bf ? run_backward<bf16_t>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, 0, 0, s, &sm, dws, dbs)
+              : run_backward<float>(d, (const char*)saved, (char*)workspace, d_h, d_c, g, 0, 0, s, &sm, dws, dbs);
+  };
+  hipStream_t st = (hipStream_t)stream;
+  if (!ptg::graphs_enabled()) return body(st);
+  ptg::Key k;
+  k.add(4).add(*d).add(x).add(x_u8).add(cin_s).add(ws).add(bs).add(saved).add(workspace).add(d_h).add(d_c)
+      .add(*g).add(dws).add(dbs).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 

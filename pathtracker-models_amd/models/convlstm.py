@@ -303,12 +303,15 @@ class ConvLSTMVideo(nn.Module):
     accepts_u8 = True
 
     def forward(self, x, testmode=False):
-        # the 1x1x1 stem + softplus in one HBM pass (pt_lstm_stem_*); a
-        # [C x 3] @ [3 x THW] library GEMM took 16 ms of a 88 ms step here
-        xbn = lstm.stem(x, self.preproc.weight, self.preproc.bias)   # [B, C, T, H, W]
-        steps = xbn.shape[2]
+        # the 1x1x1 stem + softplus written straight into the recurrence's
+        # per-step input (pt_lstm_forward_stem; r05: the f32 stem output and its
+        # layout conversions, ~3 ms of a 45 ms step, no longer exist)
+        steps = x.shape[1] if x.dtype == torch.uint8 else x.shape[2]
         want_jv = self.training and steps >= 2
-        res = self.unit1.steps(xbn, steps, want_jv=want_jv, want_seq=testmode)
+        lstm._require_device(x)
+        res = lstm.stem_steps(x, self.preproc.weight, self.preproc.bias, self.unit1.cell_weights(),
+                              ksize=self.kernel_size, dtype=self.cell_dtype, want_jv=want_jv,
+                              want_seq=testmode)
         h_t, jv = res[0], res[2]
         out = ro.readout(h_t, target_channel(x), self.readout_conv, self.target_conv,
                          self.readout_dense)                         # ptamd/readout.py

@@ -29,8 +29,8 @@ PT_LSTM_OK, PT_LSTM_ERR_ARG, PT_LSTM_ERR_UNSUPPORTED, PT_LSTM_ERR_HIP = 0, 1, 2,
 EXPORTS = ("pt_lstm_saved_bytes", "pt_lstm_workspace_bytes", "pt_lstm_forward",
            "pt_lstm_backward", "pt_lstm_jv_penalty", "pt_lstm_export_h",
            "pt_lstm_stem_workspace_bytes",
-           "pt_lstm_stem_forward", "pt_lstm_stem_backward", "pt_lstm_last_error",
-           "pt_lstm_version")
+           "pt_lstm_stem_forward", "pt_lstm_stem_backward", "pt_lstm_forward_stem",
+           "pt_lstm_backward_stem", "pt_lstm_last_error", "pt_lstm_version")
 
 _P = ctypes.c_void_p
 
@@ -126,6 +126,11 @@ def _open(path):
         lib.pt_lstm_stem_forward.argtypes = [_P, _i, _P, _P, _i, _i, _i, _ll, _P, _P]
         lib.pt_lstm_stem_backward.restype = ctypes.c_int
         lib.pt_lstm_stem_backward.argtypes = [_P, _i, _P, _P, _P, _i, _i, _i, _ll, _P, _P, _P, _P]
+        lib.pt_lstm_forward_stem.restype = ctypes.c_int
+        lib.pt_lstm_forward_stem.argtypes = [D, _P, _i, _i, _P, _P, ctypes.POINTER(Params), _P, _P, _P, _P]
+        lib.pt_lstm_backward_stem.restype = ctypes.c_int
+        lib.pt_lstm_backward_stem.argtypes = [D, _P, _i, _i, _P, _P, _P, _P, _P, _P,
+                                              ctypes.POINTER(Grads), _P, _P, _P]
         lib.pt_lstm_last_error.restype = ctypes.c_char_p
         lib.pt_lstm_version.restype = ctypes.c_char_p
         _opened[path] = lib
@@ -268,6 +273,110 @@ def run_steps(x, weights, *, ksize: int, steps: int, h0=None, c0=None, dtype: st
     """Apply ``steps`` ConvLSTM steps.  ``weights``: [Wx_i..o, bx_i..o, Wh_i..o].
     Returns (h_T, c_T, jv, h_seq) when ``want_seq``, else (h_T, c_T, jv)."""
     h, c, jv, seq = LSTMStepsFn.apply(x, h0, c0, ksize, steps, dtype, want_jv, mu, want_seq,
+                                      *weights)
+    return (h, c, jv, seq) if want_seq else (h, c, jv)
+
+
+class StemStepsFn(torch.autograd.Function):
+    """(raw clips x, stem weight, stem bias, 12 cell weights) -> (h_T, c_T, jv,
+    h_seq): ConvLSTMVideo's stem ``softplus(Conv3d 1x1x1)`` and its ``steps``
+    ConvLSTM steps (one frame per step, h0 = c0 = 0) in one library call
+    (pt_lstm_forward_stem): the stem writes the recurrence's per-step input
+    directly, so neither its f32 [B,C,T,H,W] output nor the gradient of it
+    is ever materialised.  Same values as ``stem`` followed by
+    ``run_steps`` (the stem output is rounded to the cell's storage type
+    either way); x is the f32 model input [B,cin,T,H,W] or the raw u8 clips
+    [B,T,H,W,cin] and gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, sw, sb, ksize: int, dtype: str, want_jv: bool, mu: float, want_seq: bool,
+                *weights):
+        _require_device(x)
+        if x.requires_grad:
+            raise NotImplementedError("the stem gives no gradient for its input")
+        lib = load()
+        u8 = x.dtype == torch.uint8
+        if u8:
+            b, cin_s, steps, hh, ww = x.shape[0], x.shape[-1], x.shape[1], x.shape[2], x.shape[3]
+            x = x.contiguous()
+        else:
+            b, cin_s, steps, hh, ww = x.shape
+            x = x.contiguous().float()
+        cs = sw.shape[0]
+        w = sw.detach().reshape(cs, cin_s).contiguous().float()
+        bb = sb.detach().contiguous().float()
+        weights = [wt.contiguous().float() for wt in weights]
+        ch = weights[0].shape[0]
+        d = Desc(batch=b, in_channels=cs, channels=ch, height=hh, width=ww, ksize=ksize, steps=steps,
+                 dtype=DTYPES[dtype], init_state=0, x_seq=1)
+        nsaved = lib.pt_lstm_saved_bytes(ctypes.byref(d))
+        if nsaved == 0:
+            check(1)
+        saved = torch.empty(nsaved, dtype=torch.uint8, device=x.device)
+        h_out = torch.empty((b, ch, hh, ww), dtype=torch.float32, device=x.device)
+        c_out = torch.empty_like(h_out)
+        pp = Params()
+        for g in range(4):
+            pp.wx[g] = weights[g].data_ptr()
+            pp.bx[g] = weights[4 + g].data_ptr()
+            pp.wh[g] = weights[8 + g].data_ptr()
+        st = _stream(x.device)
+        check(lib.pt_lstm_forward_stem(ctypes.byref(d), _ptr(x), int(u8), cin_s, _ptr(w), _ptr(bb),
+                                       ctypes.byref(pp), _ptr(saved), _ptr(h_out), _ptr(c_out), st))
+        jv = torch.empty((0,), device=x.device)
+        if want_jv:
+            ws = torch.empty(lib.pt_lstm_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                             device=x.device)
+            jv = torch.empty_like(h_out)
+            check(lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
+                                         _ptr(jv), st))
+        h_seq = torch.empty((b, ch, steps, hh, ww) if want_seq else (0,), device=x.device)
+        if want_seq:
+            check(lib.pt_lstm_export_h(ctypes.byref(d), _ptr(saved), _ptr(h_seq), st))
+        ctx.lib = lib
+        ctx.desc = d
+        ctx.saved_blob = saved
+        ctx.stem = (x, w, bb, int(u8), cin_s)
+        ctx.sshape = (sw.shape, sb.shape)
+        ctx.wshapes = [wt.shape for wt in weights]
+        ctx.ch = ch
+        ctx.mark_non_differentiable(jv, h_seq)
+        return h_out, c_out, jv, h_seq
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, d_h, d_c, _d_jv, _d_seq):
+        lib = ctx.lib
+        d = ctx.desc
+        x, w, bb, u8, cin_s = ctx.stem
+        dev = ctx.saved_blob.device
+        if d_h is None:
+            d_h = torch.zeros((d.batch, ctx.ch, d.height, d.width), device=dev)
+        d_h = d_h.contiguous().float()
+        d_c = d_c.contiguous().float() if d_c is not None else None
+        ws = torch.empty(lib.pt_lstm_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=dev)
+        need = ctx.needs_input_grad
+        grads = [torch.empty(s, device=dev) if need[8 + i] else None      # weights follow 8 args
+                 for i, s in enumerate(ctx.wshapes)]
+        dsw = torch.empty(ctx.sshape[0], device=dev) if need[1] else None
+        dsb = torch.empty(ctx.sshape[1], device=dev) if need[2] else None
+        gg = Grads()
+        for g in range(4):
+            gg.wx[g] = grads[g].data_ptr() if grads[g] is not None else 0
+            gg.bx[g] = grads[4 + g].data_ptr() if grads[4 + g] is not None else 0
+            gg.wh[g] = grads[8 + g].data_ptr() if grads[8 + g] is not None else 0
+        gg.d_x = gg.d_h0 = gg.d_c0 = 0
+        check(lib.pt_lstm_backward_stem(ctypes.byref(d), _ptr(x), u8, cin_s, _ptr(w), _ptr(bb),
+                                        _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_h), _ptr(d_c),
+                                        ctypes.byref(gg), _ptr(dsw), _ptr(dsb), _stream(dev)))
+        return (None, dsw, dsb, None, None, None, None, None, *grads)
+
+
+def stem_steps(x, stem_weight, stem_bias, weights, *, ksize: int, dtype: str = "f32",
+               want_jv: bool = False, mu: float = 0.9, want_seq: bool = False):
+    """The clip ConvLSTM's stem + its per-frame steps in one library call
+    (StemStepsFn).  Returns (h_T, c_T, jv, h_seq) when ``want_seq``, else (h_T, c_T, jv)."""
+    h, c, jv, seq = StemStepsFn.apply(x, stem_weight, stem_bias, ksize, dtype, want_jv, mu, want_seq,
                                       *weights)
     return (h, c, jv, seq) if want_seq else (h, c, jv)
 

@@ -243,3 +243,49 @@ def test_testmode_per_frame_outputs(dtype):
     from utils import engine
     res = engine.model_step(m, x.to(dev), "convlstm", test=True)
     assert len(res) == 3 and torch.equal(res[0], out)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("u8", [False, True])
+def test_fused_stem_equals_stem_then_steps(dtype, u8):
+    """pt_lstm_forward_stem / pt_lstm_backward_stem (r05: the stem written
+    straight into the recurrence's per-step input, its dW / db straight from
+    d x_t) against the separate pt_lstm_stem_* + pt_lstm_forward / backward
+    the model used before: the per-step input is the same values rounded the
+    same way, so logits, the Jacobian penalty and every cell gradient are
+    bitwise equal; the stem's weight / bias gradients are the same per-voxel
+    terms summed in another block order (1e-6 relative)."""
+    from ptamd import lstm
+    from ptamd import readout as ro
+    from ptamd.cell import target_channel
+    dev = _dev()
+    m = _model(7, 61).to(dev).train()
+    m.cell_dtype = dtype
+    x, y = _clips(62, 3, 6)
+    x = x.to(dev)
+    if u8:                                     # the raw clip bytes [B,T,H,W,3]
+        x = (x * 255.0).round().to(torch.uint8).permute(0, 2, 3, 4, 1).contiguous()
+    y = y.to(dev).reshape(-1, 1)
+
+    def run(fused):
+        m.zero_grad(set_to_none=True)
+        if fused:
+            out, jv = m(x)
+        else:                                  # the r04 composition of the same model
+            xbn = lstm.stem(x, m.preproc.weight, m.preproc.bias)
+            h_t, _, jv = m.unit1.steps(xbn, xbn.shape[2], want_jv=True)
+            out = ro.readout(h_t, target_channel(x), m.readout_conv, m.target_conv, m.readout_dense)
+        F.binary_cross_entropy_with_logits(out, y).backward()
+        torch.cuda.synchronize()
+        return out.detach().clone(), jv.detach().clone(), {n: p.grad.detach().clone()
+                                                           for n, p in m.named_parameters()}
+
+    o0, j0, g0 = run(False)
+    o1, j1, g1 = run(True)
+    assert torch.equal(o0, o1) and torch.equal(j0, j1)
+    for n in g0:
+        if n.startswith("preproc."):
+            err = float((g1[n] - g0[n]).abs().max())
+            assert err <= 1e-6 * float(g0[n].abs().max()) + 1e-12, (n, err)
+        else:
+            assert torch.equal(g0[n], g1[n]), n
