@@ -78,8 +78,10 @@ template <class S, int K, int RB> struct LTile {
 };
 
 struct LConvArgs {
-  const void* src;      // S [nimg][NPIX][32*NI]
-  const void* wf;       // fragments [NO][NI][K*K][KS][64]
+  const void* src;      // S [nimg][NPIX][32*NI]  (DUAL: input group 0, [nimg][NPIX][32])
+  const void* wf;       // fragments [NO][NI][K*K][KS][64]  (DUAL: group 0's, [NO][1][K*K][KS][64])
+  const void* src2;     // DUAL: input group 1, S [nimg][NPIX][32]
+  const void* wf2;      // DUAL: group 1's fragments
   float* out;           // f32 [nimg][NPIX][32*NO]
   const float* add;     // f32, same layout as out, or null
   const float* bias;    // f32 [32*NO] or null
@@ -94,8 +96,13 @@ struct LConvArgs {
 // with row reuse as in pt_device.h conv_run_k: each B fragment (tile row,
 // kw, k-step) is read from LDS once and feeds the K MFMAs of the output rows
 // it contributes to.  Wave w: output tile o = w % NO, rows (w / NO) * RW ...
-template <class S, int K, int NI, int NO, int NTH = NT>
+// DUAL (NI = 2, r05): the two input groups come from separate tensors with
+// their own fragment sets -- the per-step x-conv and h-conv of the clip
+// ConvLSTM in ONE launch, P_t = Wx x_t + Wh h_{t-1} + b, instead of an
+// all-steps x-conv whose P_t the h-conv then read back and rewrote.
+template <class S, int K, int NI, int NO, int NTH = NT, bool DUAL = false>
 __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
+  static_assert(!DUAL || NI == 2, "DUAL: two input groups");
   constexpr int NT = NTH, NWAVE = NTH / 64;   // (8 waves: the transposed conv at two waves per SIMD)
   using TT = Tr<S>;
   using F = typename TT::frag;
@@ -109,7 +116,7 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
   constexpr int NCH = L::CP / CPB;           // chunks per pixel per pass (4)
   constexpr int NCHUNK = L::TR * IMG * NCH;
   constexpr int PER = (NCHUNK + NT - 1) / NT;
-  constexpr int SRCC = 32 * NI;
+  constexpr int SRCC = DUAL ? 32 : 32 * NI;     // channels per pixel of one source tensor
   extern __shared__ __attribute__((aligned(16))) char smem[];
   S* tile = (S*)smem;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, px = lane & 31;
@@ -117,7 +124,15 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
   const int img = blockIdx.x / NBAND, band = blockIdx.x % NBAND, y0 = band * RB;
   const int o = wave % NO, r0 = (wave / NO) * RW;
   const S* src = (const S*)a.src + (size_t)img * NPIX * SRCC;
+  const S* src2 = DUAL ? (const S*)a.src2 + (size_t)img * NPIX * SRCC : nullptr;
   const F* wf = (const F*)a.wf;
+  const F* wf2 = (const F*)a.wf2;
+  // input group ig: its source pixel row base and channel offset, its fragments
+  auto gsrc = [&](int ig) { return DUAL ? (ig == 0 ? src : src2) : src + ig * 32; };
+  auto gwf = [&](int ig) {
+    return DUAL ? (ig == 0 ? wf : wf2) + (size_t)o * KK * TT::KS * 64
+                : wf + (size_t)(o * NI + ig) * KK * TT::KS * 64;
+  };
 
   for (int i = tid; i < L::BYTES / 16; i += NT) ((u32x4*)tile)[i] = u32x4{0u, 0u, 0u, 0u};
 
@@ -144,7 +159,7 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
         const int q = idx % NCH, pc = idx / NCH, col = pc % IMG, row = pc / IMG;
         const int iy = y0 + row - L::P;
         const int cy = iy < 0 ? 0 : (iy >= IMG ? IMG - 1 : iy);
-        v[k] = *(const u32x4*)(src + (size_t)(cy * IMG + col) * SRCC + ig * 32 + q * CPB);
+        v[k] = *(const u32x4*)(gsrc(ig) + (size_t)(cy * IMG + col) * SRCC + q * CPB);
         if (iy != cy) v[k] = u32x4{0u, 0u, 0u, 0u};
       }
     };
@@ -166,7 +181,7 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
     F wa[K][KSP], wb[K][KSP];
     auto ld_w = [&](int c, F (&w)[K][KSP]) {
       const int ig = c / K, kw = c - ig * K;
-      const F* wk = wf + ((size_t)((o * NI + ig) * KK + kw) * TT::KS) * 64 + lane;
+      const F* wk = gwf(ig) + (size_t)kw * TT::KS * 64 + lane;
 #pragma unroll
       for (int kh = 0; kh < K; ++kh)
 #pragma unroll
@@ -227,8 +242,7 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
         const int q = idx % NCH, pc = idx / NCH, col = pc % IMG, row = pc / IMG;
         const int iy = y0 + row - L::P;
         const int cy = iy < 0 ? 0 : (iy >= IMG ? IMG - 1 : iy);
-        v[k] = *(const u32x4*)(src + (size_t)(cy * IMG + col) * SRCC + ig * 32 + pass * L::CP +
-                               q * CPB);
+        v[k] = *(const u32x4*)(gsrc(ig) + (size_t)(cy * IMG + col) * SRCC + pass * L::CP + q * CPB);
         if (iy != cy) v[k] = u32x4{0u, 0u, 0u, 0u};
       }
       __syncthreads();   // the previous pass's fragment reads are done
@@ -244,7 +258,7 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
 
       for (int kw = 0; kw < K; ++kw) {
         F bc[K][KSP];
-        const F* wk = wf + ((size_t)((o * NI + ig) * KK + kw) * TT::KS + pass * KSP) * 64 + lane;
+        const F* wk = gwf(ig) + ((size_t)kw * TT::KS + pass * KSP) * 64 + lane;
 #pragma unroll
         for (int kh = 0; kh < K; ++kh)
 #pragma unroll
@@ -1352,7 +1366,7 @@ template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
          hipStream_t st) {
   using L = LTile<S, K, conv_rb<NO>()>;
-  LConvArgs a{src, wf, out, add, bias, nimg, lconv_fast_env()};
+  LConvArgs a{src, wf, nullptr, nullptr, out, add, bias, nimg, lconv_fast_env()};
   if constexpr (sizeof(S) == 2 && K <= 7 && NO == 1) {
     if (lconvt8_env()) {
       hipLaunchKernelGGL((k_lconv<S, K, NI, NO, 2 * NT>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(2 * NT),
@@ -1372,6 +1386,25 @@ int conv_k(int K, const void* src, const void* wf, float* out, const float* add,
            int nimg, hipStream_t st) {
   int rc = 0;
   K_SWITCH(K, (rc = conv<S, KC, NI, NO>(src, wf, out, add, bias, nimg, st)));
+  return rc;
+}
+// out = W0 * src0 + W1 * src1 + bias, the 4-gate forward with two input
+// tensors in one launch (k_lconv DUAL): the clip ConvLSTM's per-step
+// P_t = Wx x_t + Wh h_{t-1} + b
+template <class S, int K>
+int conv_dual(const void* s0, const void* w0, const void* s1, const void* w1, float* out, const float* bias,
+              int nimg, hipStream_t st) {
+  using L = LTile<S, K, conv_rb<4>()>;
+  LConvArgs a{s0, w0, s1, w1, out, nullptr, bias, nimg, lconv_fast_env()};
+  hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<4>())), dim3(NT), L::BYTES, st, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+template <class S>
+int conv_dual_k(int K, const void* s0, const void* w0, const void* s1, const void* w1, float* out,
+                const float* bias, int nimg, hipStream_t st) {
+  int rc = 0;
+  K_SWITCH(K, (rc = conv_dual<S, KC>(s0, w0, s1, w1, out, bias, nimg, st)));
   return rc;
 }
 
@@ -1409,6 +1442,7 @@ int prime_k() {
   static bool done = false;     // idempotent; a race only repeats the calls
   if (done) return 0;
   SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<4>()>::BYTES));
+  SETLDS((k_lconv<S, K, 2, 4, NT, true>), (LTile<S, K, conv_rb<4>()>::BYTES));
   SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<1>()>::BYTES));
   if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lconv<S, K, 4, 1, 2 * NT>), (LTile<S, K, conv_rb<1>()>::BYTES));
   SETLDS((k_lwgrad<S, K>), (LWBand<S, K>::BYTES));
@@ -1474,16 +1508,24 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   // static x: xg = Wx*x + b (without h0, P_0 = xg); per-step x: the
   // x-convolutions of all steps do not depend on h, so ONE launch over the
   // B*T images writes every P_t = Wx*x_t + b ([T][B] image order in xcl and P)
+  // per-step x without h0 (r05, the clip ConvLSTM): step 0's x-conv alone,
+  // then ONE launch per step for both convs (conv_dual)
+  const bool dual = p.xseq && !hinit;
   float* xg = p.xseq ? nullptr : (h0 ? (float*)(sv + p.o_xg) : P);
   if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], p.xseq ? P : xg, nullptr, pa.bias,
-                               p.xseq ? p.B * p.T : p.B, st))
+                               dual ? p.B : p.xseq ? p.B * p.T : p.B, st))
     return rc;
   for (int t = 0; t < p.T; ++t) {
     const S* hin = t == 0 ? hinit : H + (t - 1) * hstep;
-    if (hin)
+    if (dual && t > 0) {
+      if (int rc = conv_dual_k<S>(p.K, xcl + t * hstep, sv + p.o_fr[0], hin, sv + p.o_fr[1], P + t * pstep,
+                                  pa.bias, p.B, st))
+        return rc;
+    } else if (hin) {
       if (int rc = conv_k<S, 1, 4>(p.K, hin, sv + p.o_fr[1], P + t * pstep,
                                    p.xseq ? P + t * pstep : xg, nullptr, p.B, st))
         return rc;
+    }
     const float* cprev = t == 0 ? cinit : Cc + (t - 1) * hstep;
     hipLaunchKernelGGL(k_lpw_fwd<S>, grid_for((size_t)npix * 8), dim3(256), 0, st,
                        (const float*)(P + t * pstep), cprev, Cc + t * hstep, H + t * hstep, npix, p.ch);
