@@ -49,6 +49,9 @@ constexpr int KMAX = 15;
 #ifndef PT_LCONV_RB
 #define PT_LCONV_RB 4       // (experiments: 8 rows per 4-gate workgroup, one wave per SIMD)
 #endif
+#ifndef PT_LCONV_ROT
+#define PT_LCONV_ROT 1      // the column loop's weight fragments rotate in one register set
+#endif
 #ifndef PT_LCONVT_RB
 #define PT_LCONVT_RB 32     // (experiments: 16-row bands of the transposed conv, two per CU)
 #endif
@@ -134,7 +137,10 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
                 : wf + (size_t)(o * NI + ig) * KK * TT::KS * 64;
   };
 
-  for (int i = tid; i < L::BYTES / 16; i += NT) ((u32x4*)tile)[i] = u32x4{0u, 0u, 0u, 0u};
+  // DUAL: both groups' tiles are staged at the start, side by side (no
+  // mid-kernel fill: its registers, live beside two weight columns, spilled)
+  constexpr int NBUF = DUAL ? 2 : 1;
+  for (int i = tid; i < NBUF * L::BYTES / 16; i += NT) ((u32x4*)tile)[i] = u32x4{0u, 0u, 0u, 0u};
 
   f32x16 acc[RW];
 #pragma unroll
@@ -150,8 +156,8 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
   bool done = false;
   if constexpr (FAST) if (a.fast) {
     done = true;
-    u32x4 v[PER];
-    auto ld_tile = [&](int ig) {
+    u32x4 v[PER], v2[DUAL ? PER : 1];
+    auto ld_tile = [&](int ig, u32x4 (&v)[PER]) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const int idx0 = tid + k * NT;
@@ -163,21 +169,16 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
         if (iy != cy) v[k] = u32x4{0u, 0u, 0u, 0u};
       }
     };
-    auto st_tile = [&]() {
+    auto st_tile = [&](S* tl, const u32x4 (&v)[PER]) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const int idx = tid + k * NT;
         if (PER * NT == NCHUNK || idx < NCHUNK) {
           const int q = idx % NCH, pc = idx / NCH, col = pc % IMG, row = pc / IMG;
-          *(u32x4*)(tile + L::off(row, col + L::P, q * CPB)) = v[k];
+          *(u32x4*)(tl + L::off(row, col + L::P, q * CPB)) = v[k];
         }
       }
     };
-    ld_tile(0);
-    __syncthreads();                       // the clear is done
-    st_tile();
-    __syncthreads();
-    constexpr int NC = NI * K;             // (input group, kernel column) steps
     F wa[K][KSP], wb[K][KSP];
     auto ld_w = [&](int c, F (&w)[K][KSP]) {
       const int ig = c / K, kw = c - ig * K;
@@ -187,19 +188,30 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
 #pragma unroll
         for (int s2 = 0; s2 < KSP; ++s2) w[kh][s2] = wk[((size_t)kh * K * TT::KS + s2) * 64];
     };
+#if PT_LCONV_ROT
+    ld_w(0, wa);                           // (before the tile: both latencies at once, and the
+#endif                                     // column loop starts with no weight load in flight)
+    ld_tile(0, v);
+    if constexpr (DUAL) ld_tile(1, v2);
+    __syncthreads();                       // the clear is done
+    st_tile(tile, v);
+    if constexpr (DUAL) st_tile(tile + L::BYTES / sizeof(S), v2);
+    __syncthreads();
+    constexpr int NC = NI * K;             // (input group, kernel column) steps
     auto step = [&](int c, const F (&bc)[K][KSP], F (&nx)[K][KSP]) {
       const int ig = c / K, kw = c - ig * K;
       if (c + 1 < NC) ld_w(c + 1, nx);
       // (two workgroups per CU: the registers are not there, the other one covers the fill)
       constexpr bool TPF = conv_occ<NO>() == 1 && NTH == 256;
-      if (TPF && NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1);
+      if (!DUAL && TPF && NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1, v);
+      const S* tl = DUAL && ig ? tile + L::BYTES / sizeof(S) : tile;
       __builtin_amdgcn_sched_barrier(0);   // the loads go out before this column's MFMAs
       const int tcol = px + kw;
       F av[NTR][KSP];
       auto load_a = [&](int tr) {
         const int trow = r0 + tr;
 #pragma unroll
-        for (int s2 = 0; s2 < KSP; ++s2) av[tr][s2] = *(const bf16x8*)(tile + L::off(trow, tcol, 16 * s2 + 8 * h));
+        for (int s2 = 0; s2 < KSP; ++s2) av[tr][s2] = *(const bf16x8*)(tl + L::off(trow, tcol, 16 * s2 + 8 * h));
       };
       constexpr int PF = 3 < NTR ? 3 : NTR;
 #pragma unroll
@@ -216,19 +228,79 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
           }
         }
       }
-      if (NI > 1 && kw == K - 1 && ig + 1 < NI) {
-        if (!TPF) ld_tile(ig + 1);
+      if (!DUAL && NI > 1 && kw == K - 1 && ig + 1 < NI) {
+        if (!TPF) ld_tile(ig + 1, v);
         __syncthreads();                   // every wave is done with this group's tile
-        st_tile();
+        st_tile(tile, v);
         __syncthreads();
       }
     };
+#if PT_LCONV_ROT
+    // r05: ONE weight set, rotated in place -- kernel row kh's fragments are
+    // dead once output row RW - 1 has taken them (tile row kh + RW - 1), and
+    // the next column's kh fragments are loaded into the same registers there;
+    // the first use of them is tile row kh of the next column, 6 tile rows of
+    // MFMAs later.  Two sets (ping-pong) spilled the two-source conv and the
+    // 8-wave transposed conv.  Same MFMA order per accumulator.
+    (void)wb;
+#pragma unroll
+    for (int ig = 0; ig < NI; ++ig)
+#pragma unroll 1
+    for (int kw = 0; kw < K; ++kw) {
+      constexpr bool TPF = conv_occ<NO>() == 1 && NTH == 256;
+      if (!DUAL && TPF && NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1, v);
+      const S* tl = DUAL && ig ? tile + L::BYTES / sizeof(S) : tile;
+      // (after the last column: a harmless reload of group 0's first column)
+      const F* wkn = kw + 1 < K ? gwf(ig) + (size_t)(kw + 1) * TT::KS * 64 + lane
+                                : gwf(ig + 1 < NI ? ig + 1 : 0) + lane;
+      const int tcol = px + kw;
+      F av[NTR][KSP];
+      auto load_a = [&](int tr) {
+        const int trow = r0 + tr;
+#pragma unroll
+        for (int s2 = 0; s2 < KSP; ++s2) av[tr][s2] = *(const bf16x8*)(tl + L::off(trow, tcol, 16 * s2 + 8 * h));
+      };
+      constexpr int PF = 3 < NTR ? 3 : NTR;
+#pragma unroll
+      for (int tr = 0; tr < PF; ++tr) load_a(tr);
+#pragma unroll
+      for (int tr = 0; tr < NTR; ++tr) {
+        if (tr + PF < NTR) load_a(tr + PF);
+#pragma unroll
+        for (int s2 = 0; s2 < KSP; ++s2) {
+#pragma unroll
+          for (int kh = 0; kh < K; ++kh) {
+            const int i = tr - kh;
+            if (i >= 0 && i < RW) acc[i] = TT::mma(wa[kh][s2], av[tr][s2], acc[i]);
+          }
+        }
+        constexpr int RWm = RW - 1;
+        const int kd = tr - RWm;
+        if (kd >= 0 && kd < K) {
+#pragma unroll
+          for (int s2 = 0; s2 < KSP; ++s2) wa[kd][s2] = wkn[((size_t)kd * K * TT::KS + s2) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // each kernel row's reload stays where it is freed
+      }
+      if (!DUAL && NI > 1 && kw == K - 1 && ig + 1 < NI) {
+        if (!TPF) ld_tile(ig + 1, v);
+        __syncthreads();                   // every wave is done with this group's tile
+        st_tile(tile, v);
+        __syncthreads();
+      }
+    }
+#else
     ld_w(0, wa);
     for (int c = 0; c < NC; c += 2) {
       step(c, wa, wb);
       if (c + 1 < NC) step(c + 1, wb, wa);
     }
+#endif
   }
+  // (the release libraries run the column loop above for bf16 k <= 7: the
+  // plain loop is compiled in there only for the shapes that need it, so that
+  // its registers do not count against the fast one)
+  if (!FAST || PT_DIAG)
   if (!done)
   for (int ig = 0; ig < NI; ++ig) {
     for (int pass = 0; pass < TT::NPASS; ++pass) {
@@ -1396,7 +1468,7 @@ int conv_dual(const void* s0, const void* w0, const void* s1, const void* w1, fl
               int nimg, hipStream_t st) {
   using L = LTile<S, K, conv_rb<4>()>;
   LConvArgs a{s0, w0, s1, w1, out, nullptr, bias, nimg, lconv_fast_env()};
-  hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<4>())), dim3(NT), L::BYTES, st, a);
+  hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<4>())), dim3(NT), 2 * L::BYTES, st, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1442,7 +1514,7 @@ int prime_k() {
   static bool done = false;     // idempotent; a race only repeats the calls
   if (done) return 0;
   SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<4>()>::BYTES));
-  SETLDS((k_lconv<S, K, 2, 4, NT, true>), (LTile<S, K, conv_rb<4>()>::BYTES));
+  SETLDS((k_lconv<S, K, 2, 4, NT, true>), (2 * LTile<S, K, conv_rb<4>()>::BYTES));
   SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<1>()>::BYTES));
   if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lconv<S, K, 4, 1, 2 * NT>), (LTile<S, K, conv_rb<1>()>::BYTES));
   SETLDS((k_lwgrad<S, K>), (LWBand<S, K>::BYTES));

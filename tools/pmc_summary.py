@@ -20,7 +20,11 @@ import sys
 def _key(row):
     m = re.search(r"(k_[a-z_0-9]+)", row["Kernel_Name"])
     base = m.group(1) if m else row["Kernel_Name"][:50]
-    return f"{base}/wg{row['Workgroup_Size']}"
+    # template arguments (mangled Li..E / demangled <...>) keep instantiations apart
+    tail = row["Kernel_Name"][m.end():m.end() + 48] if m else ""
+    targs = re.findall(r"Li(\d+)E|Lb(\d)E|, (\d+|true|false)", tail)
+    ta = ",".join(next(x for x in t if x) for t in targs)
+    return f"{base}<{ta}>/wg{row['Workgroup_Size']}" if ta else f"{base}/wg{row['Workgroup_Size']}"
 
 
 def main():
