@@ -551,6 +551,9 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
 #ifndef PT_CONV_FLAT
 #define PT_CONV_FLAT 1
 #endif
+#ifndef PT_CONV_ROT
+#define PT_CONV_ROT 1                // register-weight pipeline: one rotating fragment set (below)
+#endif
 constexpr int WSLICE_CHUNKS = 896;   // 16-B chunks per slice: 7 taps x 2 x 64 x 16 B (bf16)
                                      //                       = 7 taps x 8 x 64 x 4 B (f32, per pass)
 constexpr int WSLICE_BYTES = WSLICE_CHUNKS * 16;
@@ -649,7 +652,13 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
   // loop below drains its prefetch at the end of every column), and the
   // column fragments alternate between two register sets (no copies).
   if constexpr (WREG && TT::NPASS == 1) {
-    F bw[2][K][KSP];
+    // PT_CONV_ROT (r05): ONE register set of column fragments, kernel row kd
+    // of column kw + 1 reloaded into bw[kd] right after output row RW - 1 has
+    // taken column kw's (step (kw, tr = kd + RW - 1)); its first use, step
+    // (kw + 1, kd), is NTR - RW + 1 steps later.  The two-set form (column
+    // kw + 1 loaded whole at the top of column kw) spilled.
+    constexpr int NSET = PT_CONV_ROT ? 1 : 2;
+    F bw[NSET][K][KSP];
     auto load_colw = [&](int kw, F (&dst)[K][KSP]) {
 #pragma unroll
       for (int kh = 0; kh < K; ++kh)
@@ -676,7 +685,7 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
       constexpr int st = decltype(c)::value;
       constexpr int kw = st / NTR, tr = st - kw * NTR;
       if constexpr (tr == 0) {
-        if constexpr (kw + 1 < K) load_colw(kw + 1, bw[(kw + 1) & 1]);
+        if constexpr (NSET == 2 && kw + 1 < K) load_colw(kw + 1, bw[(kw + 1) % NSET]);
         if constexpr (Done::prefetch_active && kw == 0) done.prefetch();
       }
       if constexpr (st + PF < NST) load_step(st + PF);
@@ -686,8 +695,13 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
 #pragma unroll
         for (int kh = 0; kh < K; ++kh) {
           const int i = tr - kh;
-          if (i >= 0 && i < RW) acc[i] = TT::mma(bw[kw & 1][kh][s], av[st % (PF + 1)][s], acc[i]);
+          if (i >= 0 && i < RW) acc[i] = TT::mma(bw[kw % NSET][kh][s], av[st % (PF + 1)][s], acc[i]);
         }
+      if constexpr (NSET == 1 && kw + 1 < K && tr >= RW - 1 && tr - (RW - 1) < K) {
+        constexpr int kd = tr - (RW - 1);
+#pragma unroll
+        for (int s = 0; s < KSP; ++s) bw[0][kd][s] = wf[((kd * K + kw + 1) * TT::KS + s) * 64 + lane];
+      }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (Done::active && kw == K - 1 && tr >= K - 1 && tr - (K - 1) < RW)
         done(tr - (K - 1), acc[tr - (K - 1)]);

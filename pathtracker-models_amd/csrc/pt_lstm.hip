@@ -58,8 +58,11 @@ constexpr int KMAX = 15;
 template <int NO> constexpr int conv_rb() { return NO == 4 ? PT_LCONV_RB : PT_LCONVT_RB; }
 // workgroups per CU the register budget allows (NO = 4: 4 rows per wave, two
 // waves per SIMD; NO = 1: 8 rows per wave over 4 input groups, one)
+#ifndef PT_LCONV_OCC
+#define PT_LCONV_OCC 2      // 4-row 4-gate workgroups per CU (r05 experiments: 3, 161 VGPRs)
+#endif
 template <int NO> constexpr int conv_occ() {
-  return NO == 4 ? (PT_LCONV_RB == 4 ? 2 : 1) : (PT_LCONVT_RB == 16 ? 2 : 1);
+  return NO == 4 ? (PT_LCONV_RB == 4 ? PT_LCONV_OCC : 1) : (PT_LCONVT_RB == 16 ? 2 : 1);
 }
 
 // ------------------------------------------------------------------ conv tile
@@ -243,12 +246,12 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
     // MFMAs later.  Two sets (ping-pong) spilled the two-source conv and the
     // 8-wave transposed conv.  Same MFMA order per accumulator.
     (void)wb;
+    constexpr bool TPF = conv_occ<NO>() == 1 && NTH == 256;
 #pragma unroll
-    for (int ig = 0; ig < NI; ++ig)
+    for (int ig = 0; ig < NI; ++ig) {
+    if (!DUAL && TPF && ig + 1 < NI) ld_tile(ig + 1, v);
 #pragma unroll 1
     for (int kw = 0; kw < K; ++kw) {
-      constexpr bool TPF = conv_occ<NO>() == 1 && NTH == 256;
-      if (!DUAL && TPF && NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1, v);
       const S* tl = DUAL && ig ? tile + L::BYTES / sizeof(S) : tile;
       // (after the last column: a harmless reload of group 0's first column)
       const F* wkn = kw + 1 < K ? gwf(ig) + (size_t)(kw + 1) * TT::KS * 64 + lane
@@ -282,12 +285,15 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);   // each kernel row's reload stays where it is freed
       }
-      if (!DUAL && NI > 1 && kw == K - 1 && ig + 1 < NI) {
-        if (!TPF) ld_tile(ig + 1, v);
-        __syncthreads();                   // every wave is done with this group's tile
-        st_tile(tile, v);
-        __syncthreads();
-      }
+    }
+    // the next input group's tile (outside the column loop: its waits then
+    // stay out of the loop head)
+    if (!DUAL && ig + 1 < NI) {
+      if (!TPF) ld_tile(ig + 1, v);
+      __syncthreads();                     // every wave is done with this group's tile
+      st_tile(tile, v);
+      __syncthreads();
+    }
     }
 #else
     ld_w(0, wa);
