@@ -1193,19 +1193,50 @@ constexpr int CONV_NT = 512;
 constexpr int BAND_ROWS = 16, BAND_NT = 256, BAND_TR = BAND_ROWS + 2 * PADMAX;
 constexpr int band_tile_bytes() { return BAND_TR * TILE * C * 2; }
 
+template <int RW>
 struct AddRowBand {
   bf16_t* out;
   const bf16_t *add0, *add1;
   size_t po;
   int h;
+  bf16x4 (&p0)[RW][4];
+  bf16x4 (&p1)[RW][4];
   static constexpr bool active = true;
   static constexpr bool prefetch_active = false;
   static constexpr bool wreg = true;
+  // r05: row i's addends are loaded PT_BAND_LEAD tile-row steps before the
+  // row's last MFMA (conv_run_k calls pre(i)), not at the row's store: the
+  // four rows of a wave finish within its last kernel column, and each store
+  // waited for its own loads in turn (XNOADD: -5.7 us of conv_bb's 39.5)
+  static constexpr int row_pre_lead = PT_BAND_LEAD;
   __device__ __forceinline__ void prefetch() const {}
+  __device__ __forceinline__ void pre(int i) const {
+    if constexpr (PT_BAND_LEAD > 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) p0[i][g] = *(const bf16x4*)(add0 + po + (size_t)i * IMG * C + 8 * g + 4 * h);
+      if (add1)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) p1[i][g] = *(const bf16x4*)(add1 + po + (size_t)i * IMG * C + 8 * g + 4 * h);
+    }
+  }
   __device__ __forceinline__ void operator()(int i, const f32x16& acc) const {
     f32x16 v = acc;
-    add_pl(add0 + po + (size_t)i * IMG * C, h, v);
-    if (add1) add_pl(add1 + po + (size_t)i * IMG * C, h, v);
+#if !PT_BAND_XNOADD     // (timing experiments only: without the addends)
+    if constexpr (PT_BAND_LEAD > 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * g + j] += (float)p0[i][g][j];
+      if (add1)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[4 * g + j] += (float)p1[i][g][j];
+    } else {
+      add_pl(add0 + po + (size_t)i * IMG * C, h, v);
+      if (add1) add_pl(add1 + po + (size_t)i * IMG * C, h, v);
+    }
+#endif
     store_pl(out + po + (size_t)i * IMG * C, h, v);
   }
 };
@@ -1251,8 +1282,12 @@ __global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a
         const int idx = i0 + k * BAND_NT < n ? i0 + k * BAND_NT : i0;
         const int pix = r0 * IMG + idx / NCH, q = idx % NCH;
         const size_t e = cb + (size_t)pix * C + q * CPB;
+#if PT_BAND_XNOFILL     // (timing experiments only: no fill loads)
+        dv[k] = make_uint4(e, 0, 0, 0); rv[k] = dv[k];
+#else
         dv[k] = *(const uint4*)(a.dc + e);
         rv[k] = *(const uint4*)(a.raw + e);
+#endif
       }
 #pragma unroll
       for (int k = 0; k < BATCH; ++k) {
@@ -1278,8 +1313,9 @@ __global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a
   f32x16 acc[RW];
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i] = zero16();
-  const AddRowBand ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
-                      cb + ((size_t)(y0 + wave * RW) * IMG + px) * C, h};
+  bf16x4 p0[RW][4], p1[RW][4];
+  const AddRowBand<RW> ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
+                          cb + ((size_t)(y0 + wave * RW) * IMG + px) * C, h, p0, p1};
   conv_run<S, PADMAX, RW, BAND_NT>(acc, fill, a.wf, tile, nullptr, a.K, wave * RW, lane, tid, a.ablate, ar);
 }
 template <class S>

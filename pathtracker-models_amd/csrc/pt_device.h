@@ -551,6 +551,15 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
 #ifndef PT_CONV_FLAT
 #define PT_CONV_FLAT 1
 #endif
+#ifndef PT_BAND_LEAD
+#define PT_BAND_LEAD 5               // banded backward conv: addend loads, tile-row steps ahead (r05: 0 / 3 / 5 = conv_bb 38.9 / 35.8 / 35.5 us)
+#endif
+#ifndef PT_BAND_XNOADD
+#define PT_BAND_XNOADD 0
+#endif
+#ifndef PT_BAND_XNOFILL
+#define PT_BAND_XNOFILL 0
+#endif
 #ifndef PT_CONV_ROT
 #define PT_CONV_ROT 1                // register-weight pipeline: one rotating fragment set (below)
 #endif
@@ -615,6 +624,16 @@ struct NoRowHook {
   static constexpr bool prefetch_active = false;
   static constexpr bool wreg = false;
 };
+
+// Row-final hooks with a per-row pre-load (row_pre_lead = L > 0): pre(i) is
+// called L tile-row steps before done(i), in the last kernel column.
+template <class D, class = void> struct RowPreLead { static constexpr int v = 0; };
+template <class D> struct RowPreLead<D, std::void_t<decltype(D::row_pre_lead)>> {
+  static constexpr int v = D::row_pre_lead;
+};
+template <class D> __device__ __forceinline__ void row_pre(const D& d, int i) {
+  if constexpr (RowPreLead<D>::v > 0) d.pre(i);
+}
 
 // Compile-time loop: fn(std::integral_constant<int, I>) for I in [I0, N), so
 // every register-array index derived from I is a constant (a #pragma unroll
@@ -701,6 +720,10 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
         constexpr int kd = tr - (RW - 1);
 #pragma unroll
         for (int s = 0; s < KSP; ++s) bw[0][kd][s] = wf[((kd * K + kw + 1) * TT::KS + s) * 64 + lane];
+      }
+      if constexpr (Done::active && RowPreLead<Done>::v > 0 && kw == K - 1) {
+        constexpr int ip = tr - (K - 1) + RowPreLead<Done>::v;
+        if constexpr (ip >= 0 && ip < RW) row_pre(done, ip);
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (Done::active && kw == K - 1 && tr >= K - 1 && tr - (K - 1) < RW)
