@@ -528,6 +528,9 @@ __global__ void k_ljv_final(const float* __restrict__ jdh, const float* __restri
 // (kh, slice): wave g owns gate g and the K taps of kernel row kh (K
 // accumulator tiles); D / X row bands are staged in LDS (double-buffered,
 // register prefetch), fragments come from ds_read_b64_tr_b16 transposed reads.
+#ifndef PT_LW_DSWZ
+#define PT_LW_DSWZ 1        // bf16 D band: chunk swizzle against 4-way bank conflicts (LWBand::dswz)
+#endif
 #ifndef PT_LW_RB
 #define PT_LW_RB 2          // bf16 D rows per weight-gradient band (r04: 2, two workgroups per CU)
 #endif
@@ -575,7 +578,18 @@ template <class S, int K> struct LWBand {
 #pragma unroll
     for (int j = 0; j < DPER; ++j) {
       const int idx = tid + j * NT;
-      *(u32x4*)(dt + idx * CPB) = d[j];
+      *(u32x4*)(dt + dswz(idx)) = d[j];
+    }
+  }
+  // bf16 (PT_LW_DSWZ, r05): the 16 16-B chunks of a D pixel XOR-swizzled by
+  // 4 * (pixel & 3), so that the four pixels of a transposed fragment read
+  // (256 B apart: one bank set) land on four bank sets -- 4-way conflicted before
+  __device__ static __forceinline__ int dswz(int idx) {     // element offset of 16-B chunk idx
+    if constexpr (sizeof(S) == 2 && PT_LW_DSWZ) {
+      const int pc = idx >> 4, q = idx & 15;
+      return pc * GC + ((q ^ ((pc & 3) << 2)) << 3);
+    } else {
+      return idx * CPB;
     }
   }
 };
@@ -673,7 +687,9 @@ __global__ __launch_bounds__(NT, 1) void k_lwgrad(LWgradArgs a) {
       };
       auto daddr = [&](int st) {
         const int yd = st >> 1, c0 = (st & 1) * 16 + 8 * hh + q;
-        return (const bf16_t*)dt + (yd * IMG + c0) * GC + g * 32 + chb;
+        // (pixel & 3) = q here and for the +4 pixel of tr_read8: one swizzle
+        const int ch = PT_LW_DSWZ ? (g * 32 + chb) ^ (q << 5) : g * 32 + chb;
+        return (const bf16_t*)dt + (yd * IMG + c0) * GC + ch;
       };
       bf16x8 av[2][K], bv[2];
       bv[0] = tr_read8<GC>(daddr(0));
