@@ -47,7 +47,7 @@ constexpr int KMAX = 15;
 // whole image for the 4-gates-in transposed conv (one output tile: each wave
 // takes 8 rows, reusing every LDS fragment across 8 output rows)
 #ifndef PT_LCONV_RB
-#define PT_LCONV_RB 4       // (experiments: 8 rows per 4-gate workgroup, one wave per SIMD)
+#define PT_LCONV_RB 4       // 4-gate rows per workgroup for f32 and k > 7 (plain column loop)
 #endif
 #ifndef PT_LCONV_ROT
 #define PT_LCONV_ROT 1      // the column loop's weight fragments rotate in one register set
@@ -55,14 +55,26 @@ constexpr int KMAX = 15;
 #ifndef PT_LCONVT_RB
 #define PT_LCONVT_RB 32     // (experiments: 16-row bands of the transposed conv, two per CU)
 #endif
-template <int NO> constexpr int conv_rb() { return NO == 4 ? PT_LCONV_RB : PT_LCONVT_RB; }
+#ifndef PT_LCONV_RB_FAST
+#define PT_LCONV_RB_FAST 8  // bf16 k <= 7 (the rotating-weight column loop): 8 rows, one wave per gate tile
+#endif
+// r05: with one rotating weight set the 8-row 4-gate workgroup fits two waves
+// per SIMD (224 VGPRs, no spills): each weight fragment feeds 8 output rows
+// instead of 4, half the L2 weight reads per MFMA (cfg3 -0.63 ms per step,
+// profiles/r05_lstmab_rb8.txt); the other shapes keep 4 rows
+template <class S, int K, int NO> constexpr int conv_rb() {
+  return NO == 4 ? (sizeof(S) == 2 && K <= 7 ? PT_LCONV_RB_FAST : PT_LCONV_RB) : PT_LCONVT_RB;
+}
 // workgroups per CU the register budget allows (NO = 4: 4 rows per wave, two
 // waves per SIMD; NO = 1: 8 rows per wave over 4 input groups, one)
+#ifndef PT_LCONVT8_DEF
+#define PT_LCONVT8_DEF 0    // the transposed conv on 8 waves x 4 rows (PT_LCONVT8 in diag builds)
+#endif
 #ifndef PT_LCONV_OCC
 #define PT_LCONV_OCC 2      // 4-row 4-gate workgroups per CU (r05 experiments: 3, 161 VGPRs)
 #endif
-template <int NO> constexpr int conv_occ() {
-  return NO == 4 ? (PT_LCONV_RB == 4 ? PT_LCONV_OCC : 1) : (PT_LCONVT_RB == 16 ? 2 : 1);
+template <class S, int K, int NO> constexpr int conv_occ() {
+  return NO == 4 ? PT_LCONV_OCC : (PT_LCONVT_RB == 16 ? 2 : 1);
 }
 
 // ------------------------------------------------------------------ conv tile
@@ -107,12 +119,12 @@ struct LConvArgs {
 // ConvLSTM in ONE launch, P_t = Wx x_t + Wh h_{t-1} + b, instead of an
 // all-steps x-conv whose P_t the h-conv then read back and rewrote.
 template <class S, int K, int NI, int NO, int NTH = NT, bool DUAL = false>
-__global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
+__global__ __launch_bounds__(NTH, (conv_occ<S, K, NO>())) void k_lconv(LConvArgs a) {
   static_assert(!DUAL || NI == 2, "DUAL: two input groups");
   constexpr int NT = NTH, NWAVE = NTH / 64;   // (8 waves: the transposed conv at two waves per SIMD)
   using TT = Tr<S>;
   using F = typename TT::frag;
-  constexpr int RB = conv_rb<NO>(), NBAND = IMG / RB;
+  constexpr int RB = conv_rb<S, K, NO>(), NBAND = IMG / RB;
   using L = LTile<S, K, RB>;
   constexpr int KK = K * K;
   constexpr int KSP = TT::KS / TT::NPASS;
@@ -205,7 +217,7 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
       const int ig = c / K, kw = c - ig * K;
       if (c + 1 < NC) ld_w(c + 1, nx);
       // (two workgroups per CU: the registers are not there, the other one covers the fill)
-      constexpr bool TPF = conv_occ<NO>() == 1 && NTH == 256;
+      constexpr bool TPF = conv_occ<S, K, NO>() == 1 && NTH == 256;
       if (!DUAL && TPF && NI > 1 && kw == 0 && ig + 1 < NI) ld_tile(ig + 1, v);
       const S* tl = DUAL && ig ? tile + L::BYTES / sizeof(S) : tile;
       __builtin_amdgcn_sched_barrier(0);   // the loads go out before this column's MFMAs
@@ -246,7 +258,7 @@ __global__ __launch_bounds__(NTH, conv_occ<NO>()) void k_lconv(LConvArgs a) {
     // MFMAs later.  Two sets (ping-pong) spilled the two-source conv and the
     // 8-wave transposed conv.  Same MFMA order per accumulator.
     (void)wb;
-    constexpr bool TPF = conv_occ<NO>() == 1 && NTH == 256;
+    constexpr bool TPF = conv_occ<S, K, NO>() == 1 && NTH == 256;
 #pragma unroll
     for (int ig = 0; ig < NI; ++ig) {
     if (!DUAL && TPF && ig + 1 < NI) ld_tile(ig + 1, v);
@@ -1455,21 +1467,21 @@ int lconv_fast_env() { return PT_SW("PT_LCONV_FAST", 1) != 0; }
 // profiles/r04_lconvt8_ab.txt): 45.83 vs 45.64 ms per step -- the 256-VGPR
 // budget spills 42 registers and the 8 waves load the same weights twice as
 // often as 4.
-int lconvt8_env() { return PT_SW("PT_LCONVT8", 0) == 1; }
+int lconvt8_env() { return PT_SW("PT_LCONVT8", PT_LCONVT8_DEF) == 1; }
 template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
          hipStream_t st) {
-  using L = LTile<S, K, conv_rb<NO>()>;
+  using L = LTile<S, K, conv_rb<S, K, NO>()>;
   LConvArgs a{src, wf, nullptr, nullptr, out, add, bias, nimg, lconv_fast_env()};
   if constexpr (sizeof(S) == 2 && K <= 7 && NO == 1) {
     if (lconvt8_env()) {
-      hipLaunchKernelGGL((k_lconv<S, K, NI, NO, 2 * NT>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(2 * NT),
+      hipLaunchKernelGGL((k_lconv<S, K, NI, NO, 2 * NT>), dim3(nimg * (IMG / conv_rb<S, K, NO>())), dim3(2 * NT),
                          L::BYTES, st, a);
       HIPCHK(hipGetLastError());
       return 0;
     }
   }
-  hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * (IMG / conv_rb<NO>())), dim3(NT),
+  hipLaunchKernelGGL((k_lconv<S, K, NI, NO>), dim3(nimg * (IMG / conv_rb<S, K, NO>())), dim3(NT),
                      L::BYTES, st, a);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1488,9 +1500,9 @@ int conv_k(int K, const void* src, const void* wf, float* out, const float* add,
 template <class S, int K>
 int conv_dual(const void* s0, const void* w0, const void* s1, const void* w1, float* out, const float* bias,
               int nimg, hipStream_t st) {
-  using L = LTile<S, K, conv_rb<4>()>;
+  using L = LTile<S, K, conv_rb<S, K, 4>()>;
   LConvArgs a{s0, w0, s1, w1, out, nullptr, bias, nimg, lconv_fast_env()};
-  hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<4>())), dim3(NT), 2 * L::BYTES, st, a);
+  hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<S, K, 4>())), dim3(NT), 2 * L::BYTES, st, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1535,10 +1547,10 @@ template <class S, int K>
 int prime_k() {
   static bool done = false;     // idempotent; a race only repeats the calls
   if (done) return 0;
-  SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<4>()>::BYTES));
-  SETLDS((k_lconv<S, K, 2, 4, NT, true>), (2 * LTile<S, K, conv_rb<4>()>::BYTES));
-  SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<1>()>::BYTES));
-  if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lconv<S, K, 4, 1, 2 * NT>), (LTile<S, K, conv_rb<1>()>::BYTES));
+  SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<S, K, 4>()>::BYTES));
+  SETLDS((k_lconv<S, K, 2, 4, NT, true>), (2 * LTile<S, K, conv_rb<S, K, 4>()>::BYTES));
+  SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<S, K, 1>()>::BYTES));
+  if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lconv<S, K, 4, 1, 2 * NT>), (LTile<S, K, conv_rb<S, K, 1>()>::BYTES));
   SETLDS((k_lwgrad<S, K>), (LWBand<S, K>::BYTES));
   if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lwgrad2<K>), (LWBand2<K>::BYTES));
   done = true;
@@ -1604,7 +1616,9 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   // B*T images writes every P_t = Wx*x_t + b ([T][B] image order in xcl and P)
   // per-step x without h0 (r05, the clip ConvLSTM): step 0's x-conv alone,
   // then ONE launch per step for both convs (conv_dual)
-  const bool dual = p.xseq && !hinit;
+  // (bf16 k > 7: the plain column loop's two-source form spills at two waves
+  // per SIMD; those shapes keep the all-steps x-conv + per-step h-conv)
+  const bool dual = p.xseq && !hinit && !(sizeof(S) == 2 && p.K > 7);
   float* xg = p.xseq ? nullptr : (h0 ? (float*)(sv + p.o_xg) : P);
   if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], p.xseq ? P : xg, nullptr, pa.bias,
                                dual ? p.B : p.xseq ? p.B * p.T : p.B, st))
