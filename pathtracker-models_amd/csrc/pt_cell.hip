@@ -1318,6 +1318,110 @@ __global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a
                           cb + ((size_t)(y0 + wave * RW) * IMG + px) * C, h, p0, p1};
   conv_run<S, PADMAX, RW, BAND_NT>(acc, fill, a.wf, tile, nullptr, a.K, wave * RW, lane, tid, a.ablate, ar);
 }
+// -------------------------------------------------------------------------
+// Staggered two-band backward conv (r05, PT_CONV_BAND=3): the two 16-row
+// bands of a clip in ONE 8-wave workgroup (both 22 x 38 tiles in LDS,
+// 107 KB).  All 8 waves fill band 0; then waves 0-3 run band 0's conv while
+// waves 4-7 fill band 1 (BN-backward loads + affine map: the HBM phase of one
+// band under the MFMA phase of the other, on the same SIMDs), sync among
+// themselves through an LDS counter and run band 1's conv.  In
+// k_conv_bwd_band the two workgroups of a CU start together and stay in step,
+// so neither fill is covered.  Per output row: k_conv_bwd_band's arithmetic
+// (same fill values, same MFMA order, same addend order): bitwise equal.
+// -------------------------------------------------------------------------
+constexpr int BAND2_NT = 512;
+constexpr int band2_lds_bytes() { return 2 * band_tile_bytes() + CONV_MISC * 4; }
+
+template <int NTH>
+__device__ __forceinline__ void band_fill(const ConvArgs<bf16_t>& a, const float* tbl, bf16_t* tile,
+                                          size_t cb, int y0, int tid) {
+  using S = bf16_t;
+  const int r0 = y0 - PADMAX < 0 ? 0 : y0 - PADMAX;
+  const int r1 = y0 + BAND_ROWS + PADMAX > IMG ? IMG : y0 + BAND_ROWS + PADMAX;
+  constexpr int CPB = 8, NCH = C / CPB;
+  const int n = (r1 - r0) * IMG * NCH;
+  constexpr int BATCH = 4;
+  for (int i0 = tid; i0 < n; i0 += BATCH * NTH) {
+    uint4 dv[BATCH], rv[BATCH];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int idx = i0 + k * NTH < n ? i0 + k * NTH : i0;
+      const int pix = r0 * IMG + idx / NCH, q = idx % NCH;
+      const size_t e = cb + (size_t)pix * C + q * CPB;
+      dv[k] = *(const uint4*)(a.dc + e);
+      rv[k] = *(const uint4*)(a.raw + e);
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int idx = i0 + k * NTH;
+      if (idx >= n) break;
+      const int pix = r0 * IMG + idx / NCH, q = idx % NCH, ch0 = q * CPB;
+      const S* rr = (const S*)&rv[k];
+      const S* dd = (const S*)&dv[k];
+      uint4 ov;
+      S* oo = (S*)&ov;
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int ch = ch0 + j;
+        oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
+      }
+      const int y = pix >> 5, x = pix & 31;
+      if (y >= y0 && y < y0 + BAND_ROWS)          // each pixel written out by one band
+        *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
+      *(uint4*)(tile + tile_off<S, PADMAX>(y - y0 + PADMAX, x + PADMAX, ch0)) = ov;
+    }
+  }
+}
+
+__global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t> a) {
+  using S = bf16_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int RW = BAND_ROWS / 4;
+  S* tile0 = (S*)smem;
+  S* tile1 = (S*)(smem + band_tile_bytes());
+  float* tbl = (float*)(smem + 2 * band_tile_bytes());
+  int* ready = (int*)(tbl + 96);            // band 1's filler waves, counted in
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, px = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x;
+  const size_t cb = clip_off(b);
+  if (tid < 32) {     // BN backward as an affine map per channel (as conv_body)
+    const double inv = 1.0 / ((double)a.bnB * NPIX);
+    double sd = 0.0, sdx = 0.0;
+    bnb_sums(a.bnb, a.bnb_ngrp, tid, sd, sdx);
+    const float md = (float)(sd * inv), mdx = (float)(sdx * inv);
+    const float mean = a.bnstat[tid], rstd = a.bnstat[32 + tid];
+    const float A = rstd * a.bnw[tid];
+    tbl[tid] = A;
+    tbl[32 + tid] = -A * mdx * rstd;
+    tbl[64 + tid] = -A * md + A * mdx * rstd * mean;
+  }
+  if (tid == 0) *ready = 0;
+  {
+    uint4* z = (uint4*)smem;
+    for (int i = tid; i < 2 * band_tile_bytes() / 16; i += BAND2_NT) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  band_fill<BAND2_NT>(a, tbl, tile0, cb, 0, tid);
+  __syncthreads();
+  const int wb = wave & 3, band = wave >> 2;
+  if (band == 1) {
+    band_fill<BAND2_NT / 2>(a, tbl, tile1, cb, BAND_ROWS, tid - BAND2_NT / 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this wave's tile stores are done
+    if (lane == 0) atomicAdd(ready, 1);
+    while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
+      __builtin_amdgcn_s_sleep(1);
+  }
+  f32x16 acc[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) acc[i] = zero16();
+  bf16x4 p0[RW][4], p1[RW][4];
+  const int y0 = band * BAND_ROWS;
+  const AddRowBand<RW> ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
+                          cb + ((size_t)(y0 + wb * RW) * IMG + px) * C, h, p0, p1};
+  conv_run_nobar<S, RW, BAND2_NT>(acc, a.wf, band ? tile1 : tile0, a.K, wb * RW, lane, tid, a.ablate, ar);
+}
+
 template <class S>
 __global__ __launch_bounds__(NT, 1) void k_bnbwd_fill(ConvArgs<S> a) {   // frame 0: BN bwd only
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -4170,6 +4274,7 @@ int set_lds_attrs() {
   SETLDS((k_conv_fwd<S, PADBIG>), (conv_lds_bytes<S, PADBIG>()));
   SETLDS((k_conv_bwd<S, PADBIG>), (conv_lds_bytes<S, PADBIG>()));
   SETLDS((k_bnbwd_fill<S>), conv_lds_bytes<S>());
+  SETLDS(k_conv_bwd_band2, band2_lds_bytes());
   SETLDS((k_pw_fa<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 0, 0>), (pwa_lds_bytes<S>()));
@@ -4230,11 +4335,19 @@ void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
 // conv pipeline k_conv_bb is equal either way (38.1 us) and the point-wise
 // kernels after it run faster (k_pw_ba 58.5 -> 56.2, k_pw_bb 71.7 -> 69.2 us,
 // interleaved; summed device time per step 23.10 -> 22.80 ms).
-int band_env() { return PT_SW("PT_CONV_BAND", 1); }
+#ifndef PT_CONV_BAND_DEF
+#define PT_CONV_BAND_DEF 3   // r05: k_conv_bwd_band2 (profiles/r05_libab_band2.txt)
+#endif
+// 3 (r05): the staggered two-band workgroup k_conv_bwd_band2
+int band_env() { return PT_SW("PT_CONV_BAND", PT_CONV_BAND_DEF); }
 template <class S>
 void launch_conv_bwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   if constexpr (sizeof(S) == 2) {
     const int bm = band_env();
+    if (bm == 3 && p.K <= 2 * PADMAX + 1 && p.ntx * p.nty == 1) {
+      hipLaunchKernelGGL(k_conv_bwd_band2, dim3(p.B), dim3(BAND2_NT), band2_lds_bytes(), st, c);
+      return;
+    }
     if ((bm == 1 || (bm == 2 && !c.add1)) && p.K <= 2 * PADMAX + 1 && p.ntx * p.nty == 1) {
       hipLaunchKernelGGL(k_conv_bwd_band, dim3(2 * p.B), dim3(BAND_NT),
                          band_tile_bytes() + CONV_MISC * 4, st, c);

@@ -649,7 +649,7 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 // k > 7 (PAD = PADBIG): the 46 x 46 tile leaves no LDS for weight slices;
 // every wave reads its column's K x KSP B fragments straight from L2 at the
 // top of the column (the ~K * RPW * KSP MFMAs of the column cover the fetch).
-template <class S, int K, int PAD, int RW, int NTH, class Fill, class Done = NoRowHook>
+template <class S, int K, int PAD, int RW, int NTH, class Fill, class Done = NoRowHook, bool BAR = true>
 __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
                                            const typename Tr<S>::frag* __restrict__ wf, S* tile,
                                            char* wbuf, int row0, int lane, int tid, int ablate,
@@ -685,9 +685,11 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
         for (int s = 0; s < KSP; ++s) dst[kh][s] = wf[((kh * K + kw) * TT::KS + s) * 64 + lane];
     };
     load_colw(0, bw[0]);
-    __syncthreads();
-    if (!(PT_ABL(ablate) & 2)) fill(0);
-    __syncthreads();
+    if constexpr (BAR) {      // (!BAR: the caller filled the tile and synchronised)
+      __syncthreads();
+      if (!(PT_ABL(ablate) & 2)) fill(0);
+      __syncthreads();
+    }
     if (PT_ABL(ablate) & 1) return;
     constexpr int NST = K * NTR;
     constexpr int PF = CONV_PF_W < NST ? CONV_PF_W : NST;
@@ -897,6 +899,22 @@ __device__ __forceinline__ void conv_run(f32x16 (&acc)[RW], Fill& fill,
       case 11: conv_run_k<S, 11, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
       default: conv_run_k<S, 9, PAD, RW, NTH>(acc, fill, wf, tile, wbuf, row0, lane, tid, ablate, done); break;
     }
+  }
+}
+
+// The register-weight pipeline without its workgroup barriers (the caller has
+// filled the tile and synchronised the waves that read it): k <= 7, bf16.
+template <class S, int RW, int NTH, class Done>
+__device__ __forceinline__ void conv_run_nobar(f32x16 (&acc)[RW], const typename Tr<S>::frag* __restrict__ wf,
+                                               S* tile, int K, int row0, int lane, int tid, int ablate,
+                                               const Done& done) {
+  static_assert(Done::wreg, "the barrier-free form is the register-weight pipeline");
+  auto nofill = [](int) {};
+  switch (K) {
+    case 7: conv_run_k<S, 7, PADMAX, RW, NTH, decltype(nofill), Done, false>(acc, nofill, wf, tile, nullptr, row0, lane, tid, ablate, done); break;
+    case 5: conv_run_k<S, 5, PADMAX, RW, NTH, decltype(nofill), Done, false>(acc, nofill, wf, tile, nullptr, row0, lane, tid, ablate, done); break;
+    case 3: conv_run_k<S, 3, PADMAX, RW, NTH, decltype(nofill), Done, false>(acc, nofill, wf, tile, nullptr, row0, lane, tid, ablate, done); break;
+    default: conv_run_k<S, 1, PADMAX, RW, NTH, decltype(nofill), Done, false>(acc, nofill, wf, tile, nullptr, row0, lane, tid, ablate, done); break;
   }
 }
 

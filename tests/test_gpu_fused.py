@@ -10,7 +10,8 @@ The persistent forward (k_persist_fwd, PT_CELL_PERSIST=1: all T frames of the
 fused segments in one launch, the BatchNorm syncs as in-launch waits on the
 deterministic group sums) is the same arithmetic in the same reduction order,
 so it too must reproduce the per-segment launches bit for bit.  So must the
-banded backward conv (PT_CONV_BAND=1): per output row the same MFMA order."""
+banded backward convs (PT_CONV_BAND=1, and the staggered two-band workgroup,
+PT_CONV_BAND=3): per output row the same MFMA order."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -55,6 +56,15 @@ def test_banded_backward_conv_is_bitwise_the_whole_clip_conv(cell, act, b, t):
     """k_conv_bwd_band (PT_CONV_BAND=1: two 16-row workgroups per clip, B
     fragments in registers) against k_conv_bwd (one workgroup per clip)."""
     _compare(cell, act, b, t, dict(fused=True, band=True))
+
+
+@pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("hgru", "softplus", 16, 6),
+                                          ("int", "softplus", 256, 64)])
+def test_staggered_two_band_conv_is_bitwise_the_whole_clip_conv(cell, act, b, t):
+    """k_conv_bwd_band2 (PT_CONV_BAND=3, r05: both bands of a clip in one
+    8-wave workgroup, band 1 filled under band 0's MFMAs, an LDS counter
+    instead of a workgroup barrier for band 1's waves) against k_conv_bwd."""
+    _compare(cell, act, b, t, dict(fused=True, band=3))
 
 
 def _compare(cell, act, b, t, other):
