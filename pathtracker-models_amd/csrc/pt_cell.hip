@@ -1956,9 +1956,9 @@ __global__ __launch_bounds__(PW_NT, 4) void k_pw_fb(CellArgs<S> a) {
 // =========================================================================
 constexpr int FUSED_NW = CONV_NT / 64, FUSED_RW = IMG / FUSED_NW;
 template <class S> constexpr int fused_lds_bytes() {
-  return tile_bytes<S, PADMAX>() + CONV_MISC * 4 + NPIX * 16 + FUSED_NW * SCR_FLOATS * 4 + 128 * 4;
+  return tile_bytes<S, PADMAX>() + CONV_MISC * 4 + NPIX * 16 + FUSED_NW * SCR_FLOATS * 4 + 128 * 4 + 8 * 4;
 }
-struct FusedLds { char* tile; float* red; f32x4* xs; float* scr; float* stat; };
+struct FusedLds { char* tile; float* red; f32x4* xs; float* scr; float* stat; int* cnt; };
 template <class S>
 __device__ __forceinline__ FusedLds fused_carve(char* smem) {
   FusedLds l;
@@ -1967,12 +1967,13 @@ __device__ __forceinline__ FusedLds fused_carve(char* smem) {
   l.xs = (f32x4*)(l.red + CONV_MISC);
   l.scr = (float*)(l.xs + NPIX);
   l.stat = l.scr + FUSED_NW * SCR_FLOATS;
+  l.cnt = (int*)(l.stat + 128);             // the staggered segments' row counters
   return l;
 }
 
 // The conv half: conv(tile, wf) for this wave's rows, rows stored as they
 // finish (out_raw), then the per-clip BN partials (bnout).
-template <class S>
+template <class S, bool NOBAR = false>
 __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<S>& c, S* out_raw,
                                            const BnSlot& bnout, char* smem, const FusedLds& L, int b,
                                            int wave, int lane, int tid, int kind) {
@@ -1983,14 +1984,51 @@ __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<
   const int h = lane >> 5, px = lane & 31;
   const StoreRow<S> sr{out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h, false};
   auto nofill = [](int) {};                 // the point-wise half filled the tile
-  conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
-                                   tid, PT_ABL(a.ablate) & 1, sr);
+  if constexpr (NOBAR)                      // (the caller waited for this wave's input rows)
+    conv_run_nobar<S, RW, CONV_NT>(acc, c.wf, (S*)L.tile, a.K, wave * RW, lane, tid, PT_ABL(a.ablate) & 1, sr);
+  else
+    conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
+                                     tid, PT_ABL(a.ablate) & 1, sr);
   PT_TR(a, kind, 4);
   if (PT_ABL(a.ablate) & 8) return;
   bn_block_stats<RW, FUSED_NW>(acc, L.red, wave, lane);       // = bn_fwd_partial, stamped
   __syncthreads();
   PT_TR(a, kind, 5);
   bn_blocks_publish<RW, FUSED_NW>(L.red, bnout, b, tid, (int*)(smem + CONV_NT * 16), (double*)smem);
+}
+
+// Staggered fused segments (r05, PT_FUSED_STAG, bf16 k <= 7): waves 0-3 (band
+// 0, conv output rows 0-15) run 3 point-wise rows each (rows 0-11), waves 4-7
+// run 5 (rows 12-31, round r of wave 4 + j is row 12 + 4 r + j), so band 0's
+// conv input (rows 0-18) is complete after waves 4-7's second round and waves
+// 0-3 start their conv while waves 4-7 are still in their point-wise rows;
+// waves 4-7 convolve once their own rows are done (band 1 needs rows 13-31
+// only).  LDS counters replace the workgroup barrier between the halves.  Per
+// row and per output row the arithmetic and the MFMA order are unchanged:
+// bitwise the unstaggered segment.
+#ifndef PT_FUSED_STAG
+#define PT_FUSED_STAG 1     // bit 0: k_fused_fb, bit 1: k_fused_fa
+#endif
+constexpr int STAG_RA = 3, STAG_RB = 5;     // point-wise rows per wave, band 0 / band 1 waves
+static_assert(4 * (STAG_RA + STAG_RB) == IMG, "staggered rows cover the frame");
+__device__ __forceinline__ int stag_rows(int wave) { return wave < 4 ? STAG_RA : STAG_RB; }
+__device__ __forceinline__ int stag_row(int wave, int i) {
+  return wave < 4 ? wave * STAG_RA + i : 4 * STAG_RA + 4 * i + (wave - 4);
+}
+// after row i of this wave is in the tile: count it (cnt[0]: band-0 waves'
+// rows, cnt[1 + i]: round i of the band-1 waves)
+__device__ __forceinline__ void stag_done(int* cnt, int wave, int i, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) atomicAdd(wave < 4 ? cnt : cnt + 1 + i, 1);
+}
+__device__ __forceinline__ void stag_wait(const int* cnt, int wave) {
+  auto ld = [&](int k) { return __hip_atomic_load(cnt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  if (wave < 4) {          // rows 0-18: all band-0 rows, band-1 rounds 0 and 1 (rows 12-19)
+    while (ld(0) < 4 * STAG_RA || ld(2) < 4) __builtin_amdgcn_s_sleep(1);
+  } else {                 // rows 13-31: every band-1 round
+    while (ld(STAG_RB) < 4) __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
 }
 
 template <class S, int ACT, int HG, bool COH>
@@ -2011,9 +2049,35 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
     bn_fwd_finalize<COH>(bnf_src(a, t - 1, 1), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat + 64,
                          b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   // this wave's first row's tiles go out before the staging and the barrier
-  FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
+  // (fa: staggered 64.1 -> 64.6 us, its heavier rows do not hide under the
+  // band-0 conv; fb 55.4 -> 52.4 us: profiles/r05_libab_fused_stag.txt)
+  constexpr bool STAG = (PT_FUSED_STAG & 2) && !COH && sizeof(S) == 2;
+  FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(STAG ? stag_row(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  if constexpr (STAG) {
+    int* cnt = L.cnt;
+    if (tid < 8) cnt[tid] = 0;
+    __syncthreads();
+    PT_TR(a, PT_K_FUSED_FA, 2);
+    const int nr = stag_rows(wave);
+#pragma unroll 1
+    for (int i = 0; i < nr; ++i) {
+      const int y = stag_row(wave, i);
+      const size_t ro = clip_off(b) + (size_t)y * IMG * C;
+      const FaIn<S> cur = nxt;
+      if (i + 1 < nr) nxt = fa_load(a, t, clip_off(b) + (size_t)stag_row(wave, i + 1) * IMG * C, cl, h);
+      if (!(PT_ABL(a.ablate) & 4))
+        fa_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
+                           (S*)L.tile);
+      stag_done(cnt, wave, i, lane);
+    }
+    stag_wait(cnt, wave);
+    PT_TR(a, PT_K_FUSED_FA, 3);
+    fused_conv<S, true>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FA);
+    PT_TR(a, PT_K_FUSED_FA, 6);
+    return;
+  }
   __syncthreads();
   PT_TR(a, PT_K_FUSED_FA, 2);
 #pragma unroll 1
@@ -2046,9 +2110,33 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
   if (!(PT_ABL(a.ablate) & 65536) && wave == FUSED_NW - 1)
     bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
                          b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
-  FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(wave * FUSED_RW) * IMG * C, cl, h);
+  constexpr bool STAG = (PT_FUSED_STAG & 1) && !COH && sizeof(S) == 2;   // (bf16: the barrier-free conv form)
+  FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(STAG ? stag_row(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  if constexpr (STAG) {
+    int* cnt = L.cnt;
+    if (tid < 8) cnt[tid] = 0;
+    __syncthreads();
+    PT_TR(a, PT_K_FUSED_FB, 2);
+    const int nr = stag_rows(wave);
+#pragma unroll 1
+    for (int i = 0; i < nr; ++i) {
+      const int y = stag_row(wave, i);
+      const size_t ro = clip_off(b) + (size_t)y * IMG * C;
+      const FbIn<S> cur = nxt;
+      if (i + 1 < nr) nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)stag_row(wave, i + 1) * IMG * C, cl, h);
+      if (!(PT_ABL(a.ablate) & 4))
+        fb_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
+                           (S*)L.tile);
+      stag_done(cnt, wave, i, lane);
+    }
+    stag_wait(cnt, wave);
+    PT_TR(a, PT_K_FUSED_FB, 3);
+    fused_conv<S, true>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FB);
+    PT_TR(a, PT_K_FUSED_FB, 6);
+    return;
+  }
   __syncthreads();
   PT_TR(a, PT_K_FUSED_FB, 2);
 #pragma unroll 1
