@@ -95,6 +95,27 @@ template <class S, int K, int RB> struct LTile {
   }
 };
 
+// The ConvLSTM point-wise forward of one (pixel, 4-channel quad) -- shared by
+// k_lpw_fwd and the two-source conv's fused epilogue, so both run the same
+// instructions.  Gates (models/convlstm.py:85-89):
+//   i = sig(P_i)  f = sig(P_f)  g = tanh(P_c)  o = sig(P_o)
+//   c' = f c + i g            h' = o tanh(c')
+__device__ __forceinline__ void lpw_fwd_quad(const f32x4& pi, const f32x4& pf, const f32x4& pg,
+                                             const f32x4& po, f32x4& c, f32x4& hn, int q, int ch) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool live = 4 * q + j < ch;
+    const float cn = sigm(pf[j]) * c[j] + sigm(pi[j]) * ftanh(pg[j]);
+    c[j] = live ? cn : 0.f;
+    hn[j] = live ? sigm(po[j]) * ftanh(cn) : 0.f;
+  }
+}
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ void st4(float* p, const f32x4& v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void st4(bf16_t* p, const f32x4& v) {
+  *(bf16x4*)p = bf16x4{(bf16_t)v[0], (bf16_t)v[1], (bf16_t)v[2], (bf16_t)v[3]};
+}
+
 struct LConvArgs {
   const void* src;      // S [nimg][NPIX][32*NI]  (DUAL: input group 0, [nimg][NPIX][32])
   const void* wf;       // fragments [NO][NI][K*K][KS][64]  (DUAL: group 0's, [NO][1][K*K][KS][64])
@@ -105,6 +126,12 @@ struct LConvArgs {
   const float* bias;    // f32 [32*NO] or null
   int nimg;
   int fast;             // bf16, k <= 7: the prefetching column loop (PT_LCONV_FAST=0: the plain one)
+  // DUAL with cout != null (r05): the step's point-wise update in the epilogue
+  // (k_lpw_fwd's arithmetic): c_t = f c_{t-1} + i g -> cout, h_t = o tanh c_t -> hout
+  const float* cprev;   // f32 [nimg][NPIX][32] or null (c_{t-1} = 0)
+  float* cout;
+  void* hout;           // S [nimg][NPIX][32]
+  int ch;               // live channels
 };
 
 // out[img][p][32 o + n] = sum_{ig, ci, tap} W[o, ig][n][ci][tap] src[img][p + tap][32 ig + ci]
@@ -386,6 +413,48 @@ __global__ __launch_bounds__(NTH, (conv_occ<S, K, NO>())) void k_lconv(LConvArgs
   }
 
   // ---- epilogue: PL layout, lane = pixel, register r = channel pl_ch(r, h)
+  if constexpr (DUAL && NO == 4 && RW % 4 == 0 && NWAVE == NO) {
+    if (a.cout) {
+      // P_t rows stored (the backward reads them), then exchanged through LDS
+      // 4 rows at a time ([row][gate][px][36]: 16-B stores conflict-free) and
+      // the point-wise step run on them: one thread per (row, pixel, quad)
+      float* xg = (float*)smem;
+      constexpr int XS = 36;
+      __syncthreads();                     // every wave is done with the tiles
+#pragma unroll
+      for (int g2 = 0; g2 < RW / 4; ++g2) {
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const int i = g2 * 4 + i4;
+          const int y = y0 + r0 + i;
+          const size_t po = ((size_t)img * NPIX + y * IMG + px) * (32 * NO) + o * 32;
+          f32x16 v = acc[i];
+          if (a.bias) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] += a.bias[o * 32 + pl_ch(r, h)];
+          }
+          store_pl(a.out + po, h, v);
+          store_pl(xg + ((i4 * 4 + o) * 32 + px) * XS, h, v);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4 * 32 * 8 / NT; ++k) {
+          const int it = tid + k * NT, i4 = it >> 8, xq = it & 255, xp = xq >> 3, q = xq & 7;
+          const float* pr = xg + (i4 * 4 * 32 + xp) * XS + 4 * q;
+          const f32x4 pi = *(const f32x4*)pr, pf = *(const f32x4*)(pr + 32 * XS),
+                      pg = *(const f32x4*)(pr + 64 * XS), pq = *(const f32x4*)(pr + 96 * XS);
+          const size_t pix = (size_t)img * NPIX + (y0 + r0 + g2 * 4 + i4) * IMG + xp;
+          f32x4 c = a.cprev ? ld4(a.cprev + pix * HC + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+          f32x4 hn;
+          lpw_fwd_quad(pi, pf, pg, pq, c, hn, q, a.ch);
+          st4(a.cout + pix * HC + 4 * q, c);
+          st4((S*)a.hout + pix * HC + 4 * q, hn);
+        }
+        __syncthreads();
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
     const int y = y0 + r0 + i;
@@ -404,12 +473,6 @@ __global__ __launch_bounds__(NTH, (conv_occ<S, K, NO>())) void k_lconv(LConvArgs
 // One thread per (pixel, 4-channel quad).  Gates (models/convlstm.py:85-89):
 //   i = sig(P_i)  f = sig(P_f)  g = tanh(P_c)  o = sig(P_o)
 //   c' = f c + i g            h' = o tanh(c')
-__device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
-__device__ __forceinline__ void st4(float* p, const f32x4& v) { *(f32x4*)p = v; }
-__device__ __forceinline__ void st4(bf16_t* p, const f32x4& v) {
-  *(bf16x4*)p = bf16x4{(bf16_t)v[0], (bf16_t)v[1], (bf16_t)v[2], (bf16_t)v[3]};
-}
-
 template <class S>
 __global__ void k_lpw_fwd(const float* __restrict__ P, const float* __restrict__ cprev,
                           float* __restrict__ cout, S* __restrict__ hout, int npix, int ch) {
@@ -420,13 +483,7 @@ __global__ void k_lpw_fwd(const float* __restrict__ P, const float* __restrict__
   const f32x4 pi = ld4(pp), pf = ld4(pp + 32), pg = ld4(pp + 64), po = ld4(pp + 96);
   f32x4 c = cprev ? ld4(cprev + (size_t)pix * HC + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 hn;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const bool live = 4 * q + j < ch;
-    const float cn = sigm(pf[j]) * c[j] + sigm(pi[j]) * ftanh(pg[j]);
-    c[j] = live ? cn : 0.f;
-    hn[j] = live ? sigm(po[j]) * ftanh(cn) : 0.f;
-  }
+  lpw_fwd_quad(pi, pf, pg, po, c, hn, q, ch);
   st4(cout + (size_t)pix * HC + 4 * q, c);
   st4(hout + (size_t)pix * HC + 4 * q, hn);
 }
@@ -1467,6 +1524,9 @@ int lconv_fast_env() { return PT_SW("PT_LCONV_FAST", 1) != 0; }
 // profiles/r04_lconvt8_ab.txt): 45.83 vs 45.64 ms per step -- the 256-VGPR
 // budget spills 42 registers and the 8 waves load the same weights twice as
 // often as 4.
+// PT_LPW_FUSE=0 (diag builds): the per-step point-wise update as its own
+// launch (k_lpw_fwd) instead of in the two-source conv's epilogue (r05)
+int lpw_fuse_env() { return PT_SW("PT_LPW_FUSE", 1) != 0; }
 int lconvt8_env() { return PT_SW("PT_LCONVT8", PT_LCONVT8_DEF) == 1; }
 template <class S, int K, int NI, int NO>
 int conv(const void* src, const void* wf, float* out, const float* add, const float* bias, int nimg,
@@ -1498,19 +1558,26 @@ int conv_k(int K, const void* src, const void* wf, float* out, const float* add,
 // tensors in one launch (k_lconv DUAL): the clip ConvLSTM's per-step
 // P_t = Wx x_t + Wh h_{t-1} + b
 template <class S, int K>
+constexpr int dual_lds_bytes() {           // both tiles, or the fused epilogue's gate exchange
+  constexpr int T2 = 2 * LTile<S, K, conv_rb<S, K, 4>()>::BYTES, XG = 4 * 4 * 32 * 36 * 4;
+  return T2 > XG ? T2 : XG;
+}
+template <class S, int K>
 int conv_dual(const void* s0, const void* w0, const void* s1, const void* w1, float* out, const float* bias,
-              int nimg, hipStream_t st) {
-  using L = LTile<S, K, conv_rb<S, K, 4>()>;
-  LConvArgs a{s0, w0, s1, w1, out, nullptr, bias, nimg, lconv_fast_env()};
-  hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<S, K, 4>())), dim3(NT), 2 * L::BYTES, st, a);
+              int nimg, hipStream_t st, const float* cprev = nullptr, float* cout = nullptr,
+              void* hout = nullptr, int ch = 0) {
+  LConvArgs a{s0, w0, s1, w1, out, nullptr, bias, nimg, lconv_fast_env(), cprev, cout, hout, ch};
+  hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<S, K, 4>())), dim3(NT),
+                     (dual_lds_bytes<S, K>()), st, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
 template <class S>
 int conv_dual_k(int K, const void* s0, const void* w0, const void* s1, const void* w1, float* out,
-                const float* bias, int nimg, hipStream_t st) {
+                const float* bias, int nimg, hipStream_t st, const float* cprev = nullptr,
+                float* cout = nullptr, void* hout = nullptr, int ch = 0) {
   int rc = 0;
-  K_SWITCH(K, (rc = conv_dual<S, KC>(s0, w0, s1, w1, out, bias, nimg, st)));
+  K_SWITCH(K, (rc = conv_dual<S, KC>(s0, w0, s1, w1, out, bias, nimg, st, cprev, cout, hout, ch)));
   return rc;
 }
 
@@ -1548,7 +1615,7 @@ int prime_k() {
   static bool done = false;     // idempotent; a race only repeats the calls
   if (done) return 0;
   SETLDS((k_lconv<S, K, 1, 4>), (LTile<S, K, conv_rb<S, K, 4>()>::BYTES));
-  SETLDS((k_lconv<S, K, 2, 4, NT, true>), (2 * LTile<S, K, conv_rb<S, K, 4>()>::BYTES));
+  SETLDS((k_lconv<S, K, 2, 4, NT, true>), (dual_lds_bytes<S, K>()));
   SETLDS((k_lconv<S, K, 4, 1>), (LTile<S, K, conv_rb<S, K, 1>()>::BYTES));
   if constexpr (sizeof(S) == 2 && K <= 7) SETLDS((k_lconv<S, K, 4, 1, 2 * NT>), (LTile<S, K, conv_rb<S, K, 1>()>::BYTES));
   SETLDS((k_lwgrad<S, K>), (LWBand<S, K>::BYTES));
@@ -1625,10 +1692,13 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
     return rc;
   for (int t = 0; t < p.T; ++t) {
     const S* hin = t == 0 ? hinit : H + (t - 1) * hstep;
-    if (dual && t > 0) {
+    if (dual && t > 0) {     // (r05) + the step's point-wise update in the conv's epilogue
+      const bool fuse = lpw_fuse_env();
       if (int rc = conv_dual_k<S>(p.K, xcl + t * hstep, sv + p.o_fr[0], hin, sv + p.o_fr[1], P + t * pstep,
-                                  pa.bias, p.B, st))
+                                  pa.bias, p.B, st, fuse ? Cc + (t - 1) * hstep : nullptr,
+                                  fuse ? Cc + t * hstep : nullptr, fuse ? H + t * hstep : nullptr, p.ch))
         return rc;
+      if (fuse) continue;
     } else if (hin) {
       if (int rc = conv_k<S, 1, 4>(p.K, hin, sv + p.o_fr[1], P + t * pstep,
                                    p.xseq ? P + t * pstep : xg, nullptr, p.B, st))
@@ -1807,7 +1877,7 @@ int pt_lstm_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params*
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
+  k.add(1).add(*d).add(x).add(*p).add(h0).add(c0).add(saved).add(h_out).add(c_out).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env()).add(lpw_fuse_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
@@ -1825,7 +1895,7 @@ int pt_lstm_backward(const pt_lstm_desc* d, const void* saved, void* workspace, 
   hipStream_t st = (hipStream_t)stream;
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
-  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
+  k.add(2).add(*d).add(saved).add(workspace).add(d_h).add(d_c).add(*g).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env()).add(lpw_fuse_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
@@ -1849,7 +1919,7 @@ int pt_lstm_forward_stem(const pt_lstm_desc* d, const void* x, int x_u8, int cin
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
   k.add(3).add(*d).add(x).add(x_u8).add(cin_s).add(ws).add(bs).add(*p).add(saved).add(h_out).add(c_out)
-      .add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
+      .add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env()).add(lpw_fuse_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 
@@ -1875,7 +1945,7 @@ int pt_lstm_backward_stem(const pt_lstm_desc* d, const void* x, int x_u8, int ci
   if (!ptg::graphs_enabled()) return body(st);
   ptg::Key k;
   k.add(4).add(*d).add(x).add(x_u8).add(cin_s).add(ws).add(bs).add(saved).add(workspace).add(d_h).add(d_c)
-      .add(*g).add(dws).add(dbs).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env());
+      .add(*g).add(dws).add(dbs).add(lconv_fast_env()).add(lwgrad2_env()).add(lconvt8_env()).add(lpw_fuse_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_LSTM_ERR_HIP, body);
 }
 

@@ -81,12 +81,14 @@ def test_video_convlstm_bf16_tolerance():
             assert cos > 0.99, (n, cos)
 
 
-@pytest.mark.parametrize("switch", ["PT_LCONV_FAST", "PT_LWGRAD2", "PT_LCONVT8"])
+@pytest.mark.parametrize("switch", ["PT_LCONV_FAST", "PT_LWGRAD2", "PT_LCONVT8", "PT_LPW_FUSE"])
 def test_lconv_prefetch_loop_is_bitwise_the_plain_loop(switch):
     """r04 bf16 k <= 7 kernels against the forms they replace, switched off per
     call: k_lconv's prefetching column loop (PT_LCONV_FAST=0: the plain loop)
     the column-owned weight gradients k_lwgrad2 (PT_LWGRAD2=1) and the
-    8-wave transposed conv (PT_LCONVT8=1), each against the default.
+    8-wave transposed conv (PT_LCONVT8=1), and (r05) the per-step point-wise
+    update in the two-source conv's epilogue against its own launch
+    (PT_LPW_FUSE=0), each against the default.
     Same MFMA order per accumulator, so logits, the Jacobian penalty and every
     gradient are bitwise equal (k=7, 5 and 3)."""
     from variants import variants

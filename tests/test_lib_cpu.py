@@ -262,7 +262,7 @@ def test_release_library_has_no_diagnostic_switches():
 # DESIGN.md §9, read only by the diagnostic builds
 CELL_SWITCHES = (b"PT_CELL_FUSED", b"PT_PWB2", b"PT_PWA2", b"PT_WG16", b"PT_WGDMA", b"PT_CELL_PERSIST",
                  b"PT_XCD_MAP", b"PT_CONV_BAND")
-LSTM_SWITCHES = (b"PT_LCONV_FAST", b"PT_LCONVT8", b"PT_LWGRAD2")
+LSTM_SWITCHES = (b"PT_LCONV_FAST", b"PT_LCONVT8", b"PT_LWGRAD2", b"PT_LPW_FUSE")
 
 
 def test_release_libraries_freeze_the_kernel_variant_switches():
