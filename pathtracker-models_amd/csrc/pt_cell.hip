@@ -2007,13 +2007,13 @@ __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<
 // row and per output row the arithmetic and the MFMA order are unchanged:
 // bitwise the unstaggered segment.
 #ifndef PT_FUSED_STAG
-#define PT_FUSED_STAG 1     // bit 0: k_fused_fb, bit 1: k_fused_fa
+#define PT_FUSED_STAG 3     // bit 0: k_fused_fb, bit 1: k_fused_fa
 #endif
-constexpr int STAG_RA = 3, STAG_RB = 5;     // point-wise rows per wave, band 0 / band 1 waves
-static_assert(4 * (STAG_RA + STAG_RB) == IMG, "staggered rows cover the frame");
-__device__ __forceinline__ int stag_rows(int wave) { return wave < 4 ? STAG_RA : STAG_RB; }
-__device__ __forceinline__ int stag_row(int wave, int i) {
-  return wave < 4 ? wave * STAG_RA + i : 4 * STAG_RA + 4 * i + (wave - 4);
+// RA point-wise rows per band-0 wave (rows 0 .. 4 RA - 1), 8 - RA per band-1
+// wave (round r of wave 4 + j: row 4 RA + 4 r + j)
+template <int RA> __device__ __forceinline__ int stag_rows(int wave) { return wave < 4 ? RA : 8 - RA; }
+template <int RA> __device__ __forceinline__ int stag_row(int wave, int i) {
+  return wave < 4 ? wave * RA + i : 4 * RA + 4 * i + (wave - 4);
 }
 // after row i of this wave is in the tile: count it (cnt[0]: band-0 waves'
 // rows, cnt[1 + i]: round i of the band-1 waves)
@@ -2021,15 +2021,27 @@ __device__ __forceinline__ void stag_done(int* cnt, int wave, int i, int lane) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) atomicAdd(wave < 4 ? cnt : cnt + 1 + i, 1);
 }
+template <int RA>
 __device__ __forceinline__ void stag_wait(const int* cnt, int wave) {
   auto ld = [&](int k) { return __hip_atomic_load(cnt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  if (wave < 4) {          // rows 0-18: all band-0 rows, band-1 rounds 0 and 1 (rows 12-19)
-    while (ld(0) < 4 * STAG_RA || ld(2) < 4) __builtin_amdgcn_s_sleep(1);
-  } else {                 // rows 13-31: every band-1 round
-    while (ld(STAG_RB) < 4) __builtin_amdgcn_s_sleep(1);
+  constexpr int RB = 8 - RA;
+  // band 0 needs image rows 0-18: every band-0 row and the band-1 rounds up
+  // to the one holding row 18; band 1 needs rows 13-31: every band-1 round
+  // and, when band-0 waves own any of rows 13-15, theirs
+  constexpr int R0 = (18 - 4 * RA) / 4;     // last band-1 round band 0 needs (RA <= 4)
+  if (wave < 4) {
+    while (ld(0) < 4 * RA || ld(1 + R0) < 4) __builtin_amdgcn_s_sleep(1);
+  } else {
+    while (ld(RB) < 4 || (4 * RA > 13 && ld(0) < 4 * RA)) __builtin_amdgcn_s_sleep(1);
   }
   asm volatile("" ::: "memory");
 }
+#ifndef PT_FUSED_STAG_RA_FA
+#define PT_FUSED_STAG_RA_FA 4
+#endif
+#ifndef PT_FUSED_STAG_RA_FB
+#define PT_FUSED_STAG_RA_FB 3
+#endif
 
 template <class S, int ACT, int HG, bool COH>
 __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvArgs<S>& c, int t, S* out_raw,
@@ -2049,10 +2061,12 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
     bn_fwd_finalize<COH>(bnf_src(a, t - 1, 1), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat + 64,
                          b == 0 ? a.bnstat + (size_t)(t - 1) * 128 + 64 : nullptr, lane);
   // this wave's first row's tiles go out before the staging and the barrier
-  // (fa: staggered 64.1 -> 64.6 us, its heavier rows do not hide under the
-  // band-0 conv; fb 55.4 -> 52.4 us: profiles/r05_libab_fused_stag.txt)
+  // (fa with 3 / 5 rows: 64.1 -> 64.6 us, its heavier rows do not hide under
+  // the band-0 conv; with 4 / 4 -- each half convolves as soon as its rows
+  // and the rows it borrows are in, no workgroup barrier -- 65.5 -> 64.2 us;
+  // fb 3 / 5: 55.4 -> 52.4 us, 4 / 4: 54.6: profiles/r05_libab_fused_stag*.txt)
   constexpr bool STAG = (PT_FUSED_STAG & 2) && !COH && sizeof(S) == 2;
-  FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(STAG ? stag_row(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
+  FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FA>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   if constexpr (STAG) {
@@ -2060,19 +2074,19 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
     if (tid < 8) cnt[tid] = 0;
     __syncthreads();
     PT_TR(a, PT_K_FUSED_FA, 2);
-    const int nr = stag_rows(wave);
+    const int nr = stag_rows<PT_FUSED_STAG_RA_FA>(wave);
 #pragma unroll 1
     for (int i = 0; i < nr; ++i) {
-      const int y = stag_row(wave, i);
+      const int y = stag_row<PT_FUSED_STAG_RA_FA>(wave, i);
       const size_t ro = clip_off(b) + (size_t)y * IMG * C;
       const FaIn<S> cur = nxt;
-      if (i + 1 < nr) nxt = fa_load(a, t, clip_off(b) + (size_t)stag_row(wave, i + 1) * IMG * C, cl, h);
+      if (i + 1 < nr) nxt = fa_load(a, t, clip_off(b) + (size_t)stag_row<PT_FUSED_STAG_RA_FA>(wave, i + 1) * IMG * C, cl, h);
       if (!(PT_ABL(a.ablate) & 4))
         fa_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, b, y, ro, cur, lane,
                            (S*)L.tile);
       stag_done(cnt, wave, i, lane);
     }
-    stag_wait(cnt, wave);
+    stag_wait<PT_FUSED_STAG_RA_FA>(cnt, wave);
     PT_TR(a, PT_K_FUSED_FA, 3);
     fused_conv<S, true>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FA);
     PT_TR(a, PT_K_FUSED_FA, 6);
@@ -2111,7 +2125,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
                          b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
   constexpr bool STAG = (PT_FUSED_STAG & 1) && !COH && sizeof(S) == 2;   // (bf16: the barrier-free conv form)
-  FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(STAG ? stag_row(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
+  FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FB>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
   if constexpr (STAG) {
@@ -2119,19 +2133,19 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     if (tid < 8) cnt[tid] = 0;
     __syncthreads();
     PT_TR(a, PT_K_FUSED_FB, 2);
-    const int nr = stag_rows(wave);
+    const int nr = stag_rows<PT_FUSED_STAG_RA_FB>(wave);
 #pragma unroll 1
     for (int i = 0; i < nr; ++i) {
-      const int y = stag_row(wave, i);
+      const int y = stag_row<PT_FUSED_STAG_RA_FB>(wave, i);
       const size_t ro = clip_off(b) + (size_t)y * IMG * C;
       const FbIn<S> cur = nxt;
-      if (i + 1 < nr) nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)stag_row(wave, i + 1) * IMG * C, cl, h);
+      if (i + 1 < nr) nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)stag_row<PT_FUSED_STAG_RA_FB>(wave, i + 1) * IMG * C, cl, h);
       if (!(PT_ABL(a.ablate) & 4))
         fb_row<S, ACT, HG>(a, t, L.stat, L.xs, y, L.scr + wave * SCR_FLOATS, y, ro, cur, lane,
                            (S*)L.tile);
       stag_done(cnt, wave, i, lane);
     }
-    stag_wait(cnt, wave);
+    stag_wait<PT_FUSED_STAG_RA_FB>(cnt, wave);
     PT_TR(a, PT_K_FUSED_FB, 3);
     fused_conv<S, true>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FB);
     PT_TR(a, PT_K_FUSED_FB, 6);
