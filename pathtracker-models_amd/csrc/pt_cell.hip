@@ -718,11 +718,24 @@ __device__ void stage_x(const void* __restrict__ xv, int xu8, f32x4* xs, int v, 
   const float* x0 = x + ((size_t)(L.b * 3 + 0) * T + t) * plane + o;
   const float* x1 = x + ((size_t)(L.b * 3 + 1) * T + t) * plane + o;
   const float* x2 = x + ((size_t)(L.b * 3 + 2) * T + t) * plane + o;
-  for (int p = tid; p < nrows * IMG; p += nthreads) {
-    const int q = (p >> 5) * W + (p & 31);
-    f32x4 v4;
-    v4[0] = x0[q]; v4[1] = x1[q]; v4[2] = x2[q]; v4[3] = 0.f;
-    xs[p] = v4;
+  // up to 4 pixels per thread in flight before the first store (one HBM
+  // round trip however many threads stage)
+  const int n = nrows * IMG;
+  for (int p0 = tid; p0 < n; p0 += 4 * nthreads) {
+    f32x4 v4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = p0 + k * nthreads;
+      if (p < n) {
+        const int q = (p >> 5) * W + (p & 31);
+        v4[k] = f32x4{x0[q], x1[q], x2[q], 0.f};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = p0 + k * nthreads;
+      if (p < n) xs[p] = v4[k];
+    }
   }
 }
 
@@ -2068,7 +2081,10 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
   constexpr bool STAG = (PT_FUSED_STAG & 2) && !COH && sizeof(S) == 2;
   FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FA>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
-  if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  // (r05) the finalising wave 7 stages no x: its BN loads and the others' x
+  // loads are one HBM round trip each, side by side
+  if (!(PT_ABL(a.ablate) & 131072) && (COH || wave < FUSED_NW - 1))
+    stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, COH ? CONV_NT : CONV_NT - 64, 1, 1);
   if constexpr (STAG) {
     int* cnt = L.cnt;
     if (tid < 8) cnt[tid] = 0;
@@ -2127,7 +2143,10 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
   constexpr bool STAG = (PT_FUSED_STAG & 1) && !COH && sizeof(S) == 2;   // (bf16: the barrier-free conv form)
   FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FB>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
-  if (!(PT_ABL(a.ablate) & 131072)) stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, CONV_NT, 1, 1);
+  // (r05) the finalising wave 7 stages no x: its BN loads and the others' x
+  // loads are one HBM round trip each, side by side
+  if (!(PT_ABL(a.ablate) & 131072) && (COH || wave < FUSED_NW - 1))
+    stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, COH ? CONV_NT : CONV_NT - 64, 1, 1);
   if constexpr (STAG) {
     int* cnt = L.cnt;
     if (tid < 8) cnt[tid] = 0;
