@@ -136,7 +136,12 @@ int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params*
  *  grads_early_event (hipEvent_t or NULL): recorded on the stream by the
  *    backward once every gradient except w_exc / w_inh is written, before the
  *    k x k weight-gradient kernel: the caller can all-reduce those gradients
- *    on another stream while that kernel runs (pt_cell_backward_dist). */
+ *    on another stream while that kernel runs (pt_cell_backward_dist).
+ *  grads_mid_event (hipEvent_t or NULL; r06): when set (and the inhibition
+ *    branch is on), the k x k weight gradients run as two launches, w_inh's
+ *    first; the event is recorded once w_inh's gradient is written, so its
+ *    all-reduce overlaps w_exc's weight-gradient kernel.  The values are the
+ *    same as with one launch (the same per-tile sums in the same order). */
 typedef int (*pt_bn_allreduce_fn)(void* user, int64_t offset, int64_t count);
 typedef struct pt_cell_dist {
     int32_t bn_world;
@@ -144,6 +149,7 @@ typedef struct pt_cell_dist {
     pt_bn_allreduce_fn allreduce;
     void* user;
     void* grads_early_event;
+    void* grads_mid_event;
 } pt_cell_dist;
 
 size_t pt_cell_bn_sync_doubles(const pt_cell_desc* d);
@@ -171,10 +177,17 @@ int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches);
 int pt_cell_timing_reset(void);
 
 /* Diagnostics: per-workgroup phase stamps (100 MHz real-time counter) of the
- * launches of frame `frame`, written to buf as u64 [PT_K_NKINDS][256][16]
- * (workgroups < 256; slot meanings in csrc/pt_cell.hip, PT_TR).  buf = NULL
+ * launches of frame `frame`, written to buf as u64 [PT_K_NKINDS][2048][32]
+ * (every (grid / 2048)-th workgroup; slot meanings in csrc/pt_cell.hip, PT_TR).  buf = NULL
  * turns it off.  hipGraph replay is off while a buffer is set. */
 int pt_cell_trace(void* buf, int frame);
+
+/* Test hook (host only, no device work): the bf16 cell's split of f32 state
+ * values into a hi plane (the bf16 operand, rounded half up in magnitude) and
+ * a lo plane (hi << 16 plus sign-extended lo == the f32 bits; a NaN keeps a
+ * quiet-NaN hi and lo = 0), exactly as the kernels store E and I (DESIGN.md
+ * §4).  No reference counterpart: the reference keeps E and I in f32. */
+int pt_cell_split_bits(const uint32_t* bits, uint16_t* hi, uint16_t* lo, int64_t n);
 
 const char* pt_last_error(void);
 const char* pt_version(void);

@@ -492,21 +492,43 @@ __device__ __forceinline__ void wg_split(int j, int nper, int B, int xmap, int& 
   else { b = j / nper; part = j % nper; }
 }
 
-// Phase stamp (diagnostics, pt_cell_trace): thread 0 of every (gridDim.x / 256)-th
-// workgroup of the traced frame writes the 100 MHz real-time counter into slot
-// `slot` (< 16) of its record trace[kind][blockIdx.x / stride][16].  Off (a
-// null pointer) in every normal run.
+// Phase stamp (diagnostics, pt_cell_trace): thread 0 of every
+// (gridDim.x / TRACE_WG)-th workgroup of the traced frame writes the 100 MHz
+// real-time counter into slot `slot` (< 32) of its record
+// trace[kind][blockIdx.x / stride][32]; the entry stamp (slot 0) also stores
+// where the workgroup runs (slot 7: XCC_ID << 32 | HW_ID: SE, SH, CU, SIMD,
+// wave slot).  PT_TRW: lane 0 of EVERY wave stamps slot base + wave (r06:
+// per-wave row ends in slots 8-15, per-wave conv ends in 16-23).  Off (a null pointer) in every normal run.
+constexpr int TRACE_WG = 2048, TRACE_SLOTS = 32;
 #if PT_DIAG
-#define PT_TR(a, kind, slot)                                                                   \
+__device__ __forceinline__ unsigned long long tr_hwid() {
+  unsigned id, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return ((unsigned long long)(xcc & 0xf) << 32) | id | (1ull << 40);
+}
+#define PT_TR_IDX(a, kind, slot)                                                               \
+  (((size_t)(kind) * TRACE_WG + blockIdx.x / (gridDim.x > TRACE_WG ? gridDim.x / TRACE_WG : 1)) * TRACE_SLOTS + (slot))
+#define PT_TR_ON(a)                                                                            \
+  ((a).trace && (a).t == (a).trace_t && blockIdx.x % (gridDim.x > TRACE_WG ? gridDim.x / TRACE_WG : 1) == 0 && \
+   blockIdx.x / (gridDim.x > TRACE_WG ? gridDim.x / TRACE_WG : 1) < TRACE_WG)
+#define PT_TR(a, kind, slot) PT_TRT(a, kind, slot, 0)
+#define PT_TRT(a, kind, slot, th)                                                              \
   do {                                                                                         \
-    const unsigned tr_s_ = gridDim.x > 256 ? gridDim.x / 256 : 1;                              \
-    if ((a).trace && (a).t == (a).trace_t && threadIdx.x == 0 && blockIdx.x % tr_s_ == 0 &&     \
-        blockIdx.x / tr_s_ < 256)                                                               \
-      (a).trace[((size_t)(kind) * 256 + blockIdx.x / tr_s_) * 16 + (slot)] =                     \
-          __builtin_amdgcn_s_memrealtime();                                                     \
+    if (PT_TR_ON(a) && threadIdx.x == (th)) {                                                  \
+      (a).trace[PT_TR_IDX(a, kind, slot)] = __builtin_amdgcn_s_memrealtime();                  \
+      if ((slot) == 0) (a).trace[PT_TR_IDX(a, kind, 7)] = tr_hwid();                           \
+    }                                                                                          \
+  } while (0)
+#define PT_TRW(a, kind, base)                                                                  \
+  do {                                                                                         \
+    if (PT_TR_ON(a) && (threadIdx.x & 63) == 0)                                                \
+      (a).trace[PT_TR_IDX(a, kind, (base) + (threadIdx.x >> 6))] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define PT_TR(a, kind, slot) do { } while (0)
+#define PT_TRT(a, kind, slot, th) do { } while (0)
+#define PT_TRW(a, kind, base) do { } while (0)
 #endif
 __device__ __forceinline__ size_t fr_off(int t, int B) { return (size_t)t * B * NPIX * C; }
 
@@ -538,7 +560,19 @@ __device__ __forceinline__ size_t clip_off(int b) { return (size_t)b * NPIX * C;
 // bits = (hi << 16) + sext(lo) exactly.  The bf16 MFMA operands taken from E
 // and I in the forward are rounded the same way (op_round), so the hi plane
 // the backward reads is the operand the forward used.
-__device__ __forceinline__ uint32_t split_hi(float v) { return (__float_as_uint(v) + 0x8000u) >> 16; }
+// NaN: the carry of the half-up add can leave a NaN's exponent
+// (0x7fff8000 -> -0.0), so a NaN's hi is its truncated bits with the quiet bit
+// forced (a NaN whose upper mantissa bits are zero would truncate to Inf) and
+// its lo is 0: NaN stays NaN in both the operand and hi + lo (payload not
+// kept); +-Inf and every finite value are unchanged (hi + lo exact).
+__host__ __device__ __forceinline__ uint32_t split_hh(uint32_t b) {
+  const uint32_t r = (b + 0x8000u) & 0xffff0000u, q = (b | 0x00400000u) & 0xffff0000u;
+  return (b & 0x7fffffffu) > 0x7f800000u ? q : r;
+}
+__host__ __device__ __forceinline__ uint16_t split_lo(uint32_t b, uint32_t hh) {
+  return (b & 0x7fffffffu) > 0x7f800000u ? (uint16_t)0 : (uint16_t)(b - hh);
+}
+__device__ __forceinline__ uint32_t split_hi(float v) { return split_hh(__float_as_uint(v)) >> 16; }
 __device__ __forceinline__ float hi_f(float v) { return __uint_as_float(split_hi(v) << 16); }
 template <class S>
 __device__ __forceinline__ f32x16 op_round(const f32x16& v) {
@@ -574,9 +608,9 @@ __device__ __forceinline__ f32x16 store_cl_split(bf16_t* __restrict__ hi, uint16
   f32x16 hv;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const uint32_t b = __float_as_uint(v[r]), hh = (b + 0x8000u) & 0xffff0000u;
+    const uint32_t b = __float_as_uint(v[r]), hh = split_hh(b);
     hp[cl_x(r, h) * C + c] = (uint16_t)(hh >> 16);
-    lo[cl_x(r, h) * C + c] = (uint16_t)(b - hh);
+    lo[cl_x(r, h) * C + c] = split_lo(b, hh);
     hv[r] = __uint_as_float(hh);
   }
   return hv;
@@ -964,6 +998,8 @@ struct ConvArgs {
   BnSlot bnout;                 // EPI_FWD: per-clip BN partials
   S* out;                       // EPI_ADD
   const S *add0, *add1;         // EPI_ADD (add1 may be null)
+  unsigned long long* trace;    // diagnostics (PT_TR): as CellArgs, stamped as trace_kind
+  int trace_t, t, trace_kind;
 };
 
 constexpr int CONV_MISC = 512;  // floats: red[256] (bn-bwd table [3][32] aliases it)
@@ -1398,6 +1434,7 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
   const size_t cb = clip_off(b);
+  PT_TR(a, a.trace_kind, 0);
   if (tid < 32) {     // BN backward as an affine map per channel (as conv_body)
     const double inv = 1.0 / ((double)a.bnB * NPIX);
     double sd = 0.0, sdx = 0.0;
@@ -1415,8 +1452,10 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
     for (int i = tid; i < 2 * band_tile_bytes() / 16; i += BAND2_NT) z[i] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
+  PT_TR(a, a.trace_kind, 1);
   band_fill<BAND2_NT>(a, tbl, tile0, cb, 0, tid);
   __syncthreads();
+  PT_TR(a, a.trace_kind, 2);
   const int wb = wave & 3, band = wave >> 2;
   if (band == 1) {
     band_fill<BAND2_NT / 2>(a, tbl, tile1, cb, BAND_ROWS, tid - BAND2_NT / 2);
@@ -1424,6 +1463,7 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
     if (lane == 0) atomicAdd(ready, 1);
     while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
       __builtin_amdgcn_s_sleep(1);
+    PT_TRT(a, a.trace_kind, 3, BAND2_NT / 2);
   }
   f32x16 acc[RW];
 #pragma unroll
@@ -1433,6 +1473,7 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
   const AddRowBand<RW> ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
                           cb + ((size_t)(y0 + wb * RW) * IMG + px) * C, h, p0, p1};
   conv_run_nobar<S, RW, BAND2_NT>(acc, a.wf, band ? tile1 : tile0, a.K, wb * RW, lane, tid, a.ablate, ar);
+  PT_TRW(a, a.trace_kind, 16);
 }
 
 template <class S>
@@ -1532,6 +1573,12 @@ __device__ __forceinline__ PLds pcarve_bb(char* smem) {
   l.slabl = (float*)p - PWB_SLAB_LO;
   return l;
 }
+// PT_EI_FULL: the bf16 cell's kappa I + gamma (forward E update,
+// k_pw_ba) and d att = dgE E_t (k_pw_ba) from the f32 values of I and E (both
+// planes) instead of their hi planes; the gate operands stay the hi planes.
+#ifndef PT_EI_FULL
+#define PT_EI_FULL 0
+#endif
 // k_pw_ba's layout.  bf16 (r05): the a_w / a_u weight gradients are formed
 // from operand tiles staged channel-major in LDS (CL rows -> [ch][128 px], the
 // PR weight-gradient contraction of pt_pr.h) by one wave per (gate, output
@@ -1736,9 +1783,10 @@ __device__ __forceinline__ FaIn<S> fa_load(const CellArgs<S>& a, int t, size_t r
   w.Iv = zero16(); w.Eo = zero16(); w.egv = zero_pk<S>(); w.cev = zero_pk<S>();
   if (t > 0) {
     // I_{t-1} feeds kappa I + gamma and the e_w gate operand: the bf16 cell
-    // reads its hi plane only (r05); E_{t-2} feeds the E update
-    // and is read in full precision
-    w.Iv = ldIh(a, t - 1, ro, c, h);
+    // reads its hi plane only (r05; PT_EI_FULL: both planes, the
+    // f32 value in kappa I + gamma, its hi rounding as the operand); E_{t-2}
+    // feeds the E update and is read in full precision
+    w.Iv = PT_EI_FULL ? ldI(a, t - 1, ro, c, h) : ldIh(a, t - 1, ro, c, h);
     if (t >= 2) w.Eo = ldE(a, t - 2, ro, c, h);
     w.egv = load_pk(a.eg + (t - 1) * fs + ro, c, h);
     w.cev = load_pk(a.ce + (t - 1) * fs + ro, c, h);
@@ -1818,7 +1866,8 @@ __device__ __forceinline__ void fa_row(const CellArgs<S>& a, int t, const float*
   } else if (a.no_inh) {
     cl_to_pa<S>(wscr, Eop, lane, pai, RND_G(a));
   } else {
-    cl_to_pa<S>(wscr, in.Iv, lane, pai, RND_G(a));
+    if constexpr (PT_EI_FULL) cl_to_pa<S>(wscr, op_round<S>(in.Iv), lane, pai, RND_G(a));
+    else cl_to_pa<S>(wscr, in.Iv, lane, pai, RND_G(a));
   }
   acc = zero16();
   acc = gemm_pa<S>(pai, a.gf[4], acc, lane);
@@ -2003,6 +2052,7 @@ __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<
     conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
                                      tid, PT_ABL(a.ablate) & 1, sr);
   PT_TR(a, kind, 4);
+  PT_TRW(a, kind, 16);
   if (PT_ABL(a.ablate) & 8) return;
   bn_block_stats<RW, FUSED_NW>(acc, L.red, wave, lane);       // = bn_fwd_partial, stamped
   __syncthreads();
@@ -2049,6 +2099,11 @@ __device__ __forceinline__ void stag_wait(const int* cnt, int wave) {
   }
   asm volatile("" ::: "memory");
 }
+// r06: the persistent forward (k_persist_fwd, COH) on the staggered segments
+// too (N2 re-measured on the r05 segments)
+#ifndef PT_PERSIST_STAG
+#define PT_PERSIST_STAG 1
+#endif
 #ifndef PT_FUSED_STAG_RA_FA
 #define PT_FUSED_STAG_RA_FA 4
 #endif
@@ -2078,7 +2133,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
   // the band-0 conv; with 4 / 4 -- each half convolves as soon as its rows
   // and the rows it borrows are in, no workgroup barrier -- 65.5 -> 64.2 us;
   // fb 3 / 5: 55.4 -> 52.4 us, 4 / 4: 54.6: profiles/r05_libab_fused_stag*.txt)
-  constexpr bool STAG = (PT_FUSED_STAG & 2) && !COH && sizeof(S) == 2;
+  constexpr bool STAG = (PT_FUSED_STAG & 2) && (!COH || PT_PERSIST_STAG) && sizeof(S) == 2;
   FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FA>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   // (r05) the finalising wave 7 stages no x: its BN loads and the others' x
@@ -2102,6 +2157,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
                            (S*)L.tile);
       stag_done(cnt, wave, i, lane);
     }
+    PT_TRW(a, PT_K_FUSED_FA, 8);
     stag_wait<PT_FUSED_STAG_RA_FA>(cnt, wave);
     PT_TR(a, PT_K_FUSED_FA, 3);
     fused_conv<S, true>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FA);
@@ -2140,7 +2196,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
   if (!(PT_ABL(a.ablate) & 65536) && wave == FUSED_NW - 1)
     bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
                          b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
-  constexpr bool STAG = (PT_FUSED_STAG & 1) && !COH && sizeof(S) == 2;   // (bf16: the barrier-free conv form)
+  constexpr bool STAG = (PT_FUSED_STAG & 1) && (!COH || PT_PERSIST_STAG) && sizeof(S) == 2;   // (bf16: the barrier-free conv form)
   FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FB>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   // (r05) the finalising wave 7 stages no x: its BN loads and the others' x
@@ -2164,6 +2220,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
                            (S*)L.tile);
       stag_done(cnt, wave, i, lane);
     }
+    PT_TRW(a, PT_K_FUSED_FB, 8);
     stag_wait<PT_FUSED_STAG_RA_FB>(cnt, wave);
     PT_TR(a, PT_K_FUSED_FB, 3);
     fused_conv<S, true>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FB);
@@ -2307,8 +2364,11 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
       if (head || HG) {
         const f32x16 dgE = head ? load_cl(dgsrc + ro, c, h) : zero16();
         const Pk<S> dAt = HG ? load_pk(a.dAt + ro, c, h) : zero_pk<S>();
-        // E_t as the a_u gate operand and in d att = dgE E_t: the hi plane (bf16 cell)
-        const f32x16 Et = head ? ldEh(a, t, ro, c, h) : zero16();
+        // E_t as the a_u gate operand and in d att = dgE E_t: the hi plane
+        // (bf16 cell; PT_EI_FULL: d att from the f32 value, as the forward's
+        // gE = att E_t)
+        const f32x16 Ef = head ? (PT_EI_FULL ? ldE(a, t, ro, c, h) : ldEh(a, t, ro, c, h)) : zero16();
+        const f32x16 Et = PT_EI_FULL ? op_round<S>(Ef) : Ef;
         F pax[Tr<S>::KS], pae[Tr<S>::KS];
         cl_to_pa<S>(wscr, xv, lane, pax, RND_G(a));
         cl_to_pa<S>(wscr, Et, lane, pae, RND_G(a));
@@ -2319,7 +2379,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           att[r] = sigm_b(g[r], nba);
-          const float datt = HG ? dgE[r] * Et[r] + (float)dAt[r] : dgE[r] * Et[r];
+          const float datt = HG ? dgE[r] * Ef[r] + (float)dAt[r] : dgE[r] * Ef[r];
           dap[r] = datt * att[r] * (1.f - att[r]);
           sm[0] += dap[r];
         }
@@ -2353,7 +2413,8 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
       GE = load_cl(a.GEfin + ro, c, h);
     }
     if (head) {
-      const f32x16 Iv = ldIh(a, t, ro, c, h);      // kappa I + gamma as the forward formed it
+      // kappa I + gamma as the forward formed it
+      const f32x16 Iv = PT_EI_FULL ? ldI(a, t, ro, c, h) : ldIh(a, t, ro, c, h);
       const f32x16 cev = load_cl(a.ce + t * fs + ro, c, h);
       const f32x16 egv = load_cl(a.eg + t * fs + ro, c, h);
       const f32x16 Eo = t > 0 ? ldE(a, t - 1, ro, c, h) : zero16();   // full: eh - E_{t-1}
@@ -2404,6 +2465,7 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   sm[3] = bs1;   // d bn1.weight = sum dy * xhat
   sm[4] = bs0;   // d bn1.bias   = sum dy
   PT_TR(a, PT_K_PW_BA, 3);
+  PT_TRW(a, PT_K_PW_BA, 8);
   const bool bn = head && !(PT_ABL(a.ablate) & 8);
   const BnSlot bo = bnb_slot(a, t, 1, B * PWA_WGPC);
   float bv = 0.f;
@@ -2938,6 +3000,7 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
   if constexpr (NSET > 3) set_body(3, in1);
   static_assert(NSET <= 4, "set bodies");
   PT_TR(a, PT_K_PW_BB, 3);
+  PT_TRW(a, PT_K_PW_BB, 8);
   if (do_wg) {                            // the gate tiles' old slab values
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -3931,7 +3994,10 @@ __global__ void k_reduce(ReduceArgs r) {
   const int KK = r.K * r.K;
   const int n_small = SLAB;                  // slab entries
   const int n_w = 2 * KK * 1024;             // conv weights
-  const int e0 = r.part == 0 ? 0 : n_small, e1 = r.part == 0 ? n_small : n_small + n_w;
+  // part 1: both k x k weights; 2: w_inh only; 3: w_exc only (the three-part
+  // gradient exchange, pt_cell_dist.grads_mid_event)
+  const int e0 = r.part == 0 ? 0 : n_small + (r.part == 3 ? KK * 1024 : 0);
+  const int e1 = r.part == 0 ? n_small : n_small + (r.part == 2 ? KK * 1024 : n_w);
   for (int e = e0 + blockIdx.x * blockDim.x + threadIdx.x; e < e1; e += gridDim.x * blockDim.x) {
     if (e < n_small) {
       const float s = strided_sum(r.slab + e, SLAB, r.B);
@@ -4489,6 +4555,7 @@ ConvArgs<S> conv_args(const CellArgs<S>& a) {
   c.bnB = a.B * a.bn_world;
   c.ntx = a.ntx; c.nty = a.nty;
   c.xmap = a.xmap;
+  c.trace = a.trace; c.trace_t = a.trace_t; c.t = a.t;
   return c;
 }
 
@@ -4528,7 +4595,10 @@ bool use_fused(const pt_cell_desc* d, const Plan& p) {
 // Persistent forward (k_persist_fwd): opt-in (PT_CELL_PERSIST=1, read per
 // call) on the fused configurations without SyncBN, and only when the B
 // workgroups are all resident at once (occupancy x CUs, checked per device).
-bool persist_env() { return PT_SW("PT_CELL_PERSIST", 0) == 1; }
+#ifndef PT_PERSIST_DEF
+#define PT_PERSIST_DEF 0     // A/B builds (tools/libab.py): the persistent forward by default
+#endif
+bool persist_env() { return PT_SW("PT_CELL_PERSIST", PT_PERSIST_DEF) == 1; }
 template <class S>
 bool persist_fits(int B) {
   static int cap[2] = {-1, -1};           // per storage type; one device per process
@@ -4665,14 +4735,17 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   return 0;
 }
 
-// The backward in two phases: 0 = the BPTT sweep and every gradient except
+// The backward in phases: 0 = the BPTT sweep and every gradient except
 // the two k x k weights (k_reduce part 0); 1 = k_wgrad and those two (part 1).
 // pt_cell_dist.grads_early_event is recorded between them, so the caller can
-// all-reduce the early gradients on another stream while k_wgrad runs.
+// all-reduce the early gradients on another stream while k_wgrad runs.  With
+// grads_mid_event (r06) phase 1 is split by weight: 1 = k_wgrad of w_inh
+// alone and its reduction (part 2), the event, then 2 = w_exc (part 3), so
+// w_inh's all-reduce runs under w_exc's weight gradient.
 template <class S>
 int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
                  const void* saved, void* ws, const float* d_e_last, const pt_cell_grads* g,
-                 const pt_cell_dist* dist, int phase, hipStream_t st) {
+                 const pt_cell_dist* dist, int phase, hipStream_t st, bool wsplit = false) {
   const Plan p = plan(d);
   if (int rc = set_lds_attrs<S>()) return rc;
   pt_cell_params padded;
@@ -4693,12 +4766,13 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   if (d->no_inh) { r.g.w_inh = nullptr; r.g.alpha = nullptr; r.g.mu = nullptr;
                    r.g.bn_w[0] = nullptr; r.g.bn_b[0] = nullptr;
                    r.g.gate_w[2] = r.g.gate_w[3] = nullptr; r.g.gate_b[2] = r.g.gate_b[3] = nullptr; }
-  if (phase == 1) {
+  if (phase >= 1) {
     float* wslab = (float*)((char*)ws + p.o_wslab);
-    const int conv0 = d->no_inh ? 1 : 0;
+    // the weights this phase forms: [conv0, conv1]
+    const int conv0 = wsplit ? phase - 1 : d->no_inh ? 1 : 0, conv1 = wsplit ? phase - 1 : 1;
     if (d->no_inh) HIPCHK(zero_async(wslab, (size_t)p.nwg * p.K * p.K * 1024 * 4, st));
     timed(PT_K_WGRAD, st, [&] {
-      const dim3 grid(p.nwg, 2 - conv0, wgrad_groups(p.K, sizeof(S) == 2));
+      const dim3 grid(p.nwg, conv1 - conv0 + 1, wgrad_groups(p.K, sizeof(S) == 2));
       if constexpr (sizeof(S) == 2)
         if (p.K == 7 && wg16_env()) {
           if (wgdma_env())
@@ -4715,8 +4789,8 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       else
         hipLaunchKernelGGL((k_wgrad<S, PADBIG>), grid, dim3(NT), (wgrad_lds_bytes<S, PADBIG>()), st, a,
                            wslab, p.nwg, conv0); });
-    r.part = 1;
-    const int n_w = 2 * p.K * p.K * 1024;                     // one thread per output element
+    r.part = wsplit ? 1 + phase : 1;
+    const int n_w = (wsplit ? 1 : 2) * p.K * p.K * 1024;      // one thread per output element
     timed(PT_K_REDUCE, st, [&] {
       hipLaunchKernelGGL(k_reduce, dim3((n_w + 255) / 256), dim3(256), 0, st, r); });
     HIPCHK(hipGetLastError());
@@ -4764,6 +4838,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   for (int t = p.T - 1; t >= 0; --t) {
     // dI_t = conv^T(BN1-bwd(dcE), w_exc) + dI_local + dI from frame t+1
     ConvArgs<S> cb = conv_args(a);
+    cb.t = t; cb.trace_kind = PT_K_CONV_BB;
     cb.dc = a.dcE; cb.raw = a.ce + t * fs; cb.bnstat = bst + (size_t)t * 128 + 64;
     bwd_src(cb, t, 1, nprod_a);
     cb.bnw = a.bnw1; cb.fill_out = a.dce_s + t * fs;
@@ -4782,6 +4857,7 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       if (int rc = sync_bwd(t, 0, nprod_b)) return rc;
       // dgE_t = conv^T(BN0-bwd(dcI), w_inh) + e_u^T d_e_pre ; frame 0's conv^T is dead (E_{-1}=0)
       ConvArgs<S> ca = conv_args(a);
+      ca.t = t; ca.trace_kind = PT_K_CONV_BA;
       ca.dc = a.dcI; ca.raw = a.ci + t * fs; ca.bnstat = bst + (size_t)t * 128;
       bwd_src(ca, t, 0, nprod_b);
       ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
@@ -4898,10 +4974,12 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
   hipStream_t st = (hipStream_t)stream;
   const bool bf = d->dtype == PT_DTYPE_BF16;
   const hipEvent_t early = dist ? (hipEvent_t)dist->grads_early_event : nullptr;
-  for (int phase = 0; phase < 2; ++phase) {
+  const hipEvent_t mid = dist ? (hipEvent_t)dist->grads_mid_event : nullptr;
+  const bool wsplit = mid && !d->no_inh;     // three phases: sweep, w_inh, w_exc
+  for (int phase = 0; phase < (wsplit ? 3 : 2); ++phase) {
     auto body = [&](hipStream_t s) {
-      return bf ? run_backward<bf16_t>(d, x, p, saved, ws, d_e_last, g, dist, phase, s)
-                : run_backward<float>(d, x, p, saved, ws, d_e_last, g, dist, phase, s);
+      return bf ? run_backward<bf16_t>(d, x, p, saved, ws, d_e_last, g, dist, phase, s, wsplit)
+                : run_backward<float>(d, x, p, saved, ws, d_e_last, g, dist, phase, s, wsplit);
     };
     int rc;
     if (!use_graph() || syncbn(dist)) {
@@ -4909,12 +4987,13 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
     } else {
       if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
       ptg::Key k;
-      k.add(phase).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
+      k.add(phase).add(wsplit).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
           .add(band_env()).add(pwb2_env()).add(pwa2_env()).add(xmap_env()).add(wg16_env()).add(wgdma_env());
       rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
     }
     if (rc) return rc;
     if (phase == 0 && early) HIPCHK(hipEventRecord(early, st));
+    if (phase == 1 && wsplit) HIPCHK(hipEventRecord(mid, st));
   }
   return 0;
 }
@@ -4923,6 +5002,16 @@ int pt_cell_backward(const pt_cell_desc* d, const void* x, const pt_cell_params*
                      const void* saved, void* ws, const float* d_e_last, const pt_cell_grads* g,
                      pt_stream_t stream) {
   return pt_cell_backward_dist(d, x, p, saved, ws, d_e_last, g, nullptr, stream);
+}
+
+int pt_cell_split_bits(const uint32_t* bits, uint16_t* hi, uint16_t* lo, int64_t n) {
+  if (!bits || !hi || !lo || n < 0) return fail(PT_ERR_ARG, "pt_cell_split_bits: null buffer or n < 0%s%ld");
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t hh = split_hh(bits[i]);
+    hi[i] = (uint16_t)(hh >> 16);
+    lo[i] = split_lo(bits[i], hh);
+  }
+  return 0;
 }
 
 int pt_cell_trace(void* buf, int frame) {

@@ -65,6 +65,14 @@ constexpr int KMAX = 15;
 template <class S, int K, int NO> constexpr int conv_rb() {
   return NO == 4 ? (sizeof(S) == 2 && K <= 7 ? PT_LCONV_RB_FAST : PT_LCONV_RB) : PT_LCONVT_RB;
 }
+// The two-source conv (DUAL) runs the step's point-wise update in its epilogue
+// only for the shapes whose epilogue exchange is written for: four gate tiles
+// on four waves and a multiple of 4 output rows per wave.  The host passes the
+// c / h outputs only to those instantiations (conv_dual), and skips the
+// separate k_lpw_fwd launch only when it did.
+template <class S, int K, int NTH> constexpr bool dual_fuses() {
+  return NTH / 64 == 4 && (conv_rb<S, K, 4>() * 4 / (NTH / 64)) % 4 == 0;
+}
 // workgroups per CU the register budget allows (NO = 4: 4 rows per wave, two
 // waves per SIMD; NO = 1: 8 rows per wave over 4 input groups, one)
 #ifndef PT_LCONVT8_DEF
@@ -413,7 +421,8 @@ __global__ __launch_bounds__(NTH, (conv_occ<S, K, NO>())) void k_lconv(LConvArgs
   }
 
   // ---- epilogue: PL layout, lane = pixel, register r = channel pl_ch(r, h)
-  if constexpr (DUAL && NO == 4 && RW % 4 == 0 && NWAVE == NO) {
+  if constexpr (DUAL && dual_fuses<S, K, NTH>()) {
+    static_assert(NO == 4 && RW % 4 == 0 && NWAVE == NO && (4 * 32 * 8) % NT == 0, "fused epilogue shape");
     if (a.cout) {
       // P_t rows stored (the backward reads them), then exchanged through LDS
       // 4 rows at a time ([row][gate][px][36]: 16-B stores conflict-free) and
@@ -455,6 +464,8 @@ __global__ __launch_bounds__(NTH, (conv_occ<S, K, NO>())) void k_lconv(LConvArgs
       return;
     }
   }
+  if constexpr (DUAL && !dual_fuses<S, K, NTH>())
+    if (a.cout) __builtin_trap();          // the host never passes c / h outputs here
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
     const int y = y0 + r0 + i;
@@ -1565,8 +1576,11 @@ constexpr int dual_lds_bytes() {           // both tiles, or the fused epilogue'
 template <class S, int K>
 int conv_dual(const void* s0, const void* w0, const void* s1, const void* w1, float* out, const float* bias,
               int nimg, hipStream_t st, const float* cprev = nullptr, float* cout = nullptr,
-              void* hout = nullptr, int ch = 0) {
-  LConvArgs a{s0, w0, s1, w1, out, nullptr, bias, nimg, lconv_fast_env(), cprev, cout, hout, ch};
+              void* hout = nullptr, int ch = 0, bool* fused = nullptr) {
+  const bool f = cout && dual_fuses<S, K, NT>();
+  if (fused) *fused = f;
+  LConvArgs a{s0, w0, s1, w1, out, nullptr, bias, nimg, lconv_fast_env(), f ? cprev : nullptr,
+              f ? cout : nullptr, f ? hout : nullptr, ch};
   hipLaunchKernelGGL((k_lconv<S, K, 2, 4, NT, true>), dim3(nimg * (IMG / conv_rb<S, K, 4>())), dim3(NT),
                      (dual_lds_bytes<S, K>()), st, a);
   HIPCHK(hipGetLastError());
@@ -1575,9 +1589,9 @@ int conv_dual(const void* s0, const void* w0, const void* s1, const void* w1, fl
 template <class S>
 int conv_dual_k(int K, const void* s0, const void* w0, const void* s1, const void* w1, float* out,
                 const float* bias, int nimg, hipStream_t st, const float* cprev = nullptr,
-                float* cout = nullptr, void* hout = nullptr, int ch = 0) {
+                float* cout = nullptr, void* hout = nullptr, int ch = 0, bool* fused = nullptr) {
   int rc = 0;
-  K_SWITCH(K, (rc = conv_dual<S, KC>(s0, w0, s1, w1, out, bias, nimg, st, cprev, cout, hout, ch)));
+  K_SWITCH(K, (rc = conv_dual<S, KC>(s0, w0, s1, w1, out, bias, nimg, st, cprev, cout, hout, ch, fused)));
   return rc;
 }
 
@@ -1694,11 +1708,13 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
     const S* hin = t == 0 ? hinit : H + (t - 1) * hstep;
     if (dual && t > 0) {     // (r05) + the step's point-wise update in the conv's epilogue
       const bool fuse = lpw_fuse_env();
+      bool fused = false;      // the instantiation ran the update (dual_fuses)
       if (int rc = conv_dual_k<S>(p.K, xcl + t * hstep, sv + p.o_fr[0], hin, sv + p.o_fr[1], P + t * pstep,
                                   pa.bias, p.B, st, fuse ? Cc + (t - 1) * hstep : nullptr,
-                                  fuse ? Cc + t * hstep : nullptr, fuse ? H + t * hstep : nullptr, p.ch))
+                                  fuse ? Cc + t * hstep : nullptr, fuse ? H + t * hstep : nullptr, p.ch,
+                                  &fused))
         return rc;
-      if (fuse) continue;
+      if (fused) continue;
     } else if (hin) {
       if (int rc = conv_k<S, 1, 4>(p.K, hin, sv + p.o_fr[1], P + t * pstep,
                                    p.xseq ? P + t * pstep : xg, nullptr, p.B, st))

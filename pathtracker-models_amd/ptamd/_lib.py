@@ -28,13 +28,15 @@ PT_X_F32_NCTHW, PT_X_U8_NTHWC = 0, 1
 EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
            "pt_cell_export_exc", "pt_cell_backward", "pt_cell_bn_sync_doubles",
            "pt_cell_forward_dist", "pt_cell_backward_dist", "pt_cell_timing_enable",
-           "pt_cell_timing_read", "pt_cell_timing_reset", "pt_cell_trace", "pt_last_error", "pt_version")
+           "pt_cell_timing_read", "pt_cell_timing_reset", "pt_cell_trace", "pt_cell_split_bits",
+           "pt_last_error", "pt_version")
 
 # kernel kinds for pt_cell_timing_* (include/pt_cell.h)
 KIND_NAMES = ("k_pw_fa", "k_conv_fa", "k_pw_fb", "k_conv_fb", "k_pw_ba", "k_conv_ba",
               "k_pw_bb", "k_conv_bb", "k_wgrad", "k_prep", "k_reduce", "k_fused_fa",
               "k_fused_fb", "k_persist_fwd")
 NKINDS = len(KIND_NAMES)
+TRACE_WG, TRACE_SLOTS = 2048, 32      # pt_cell_trace record layout (csrc/pt_cell.hip PT_TR)
 
 _P = ctypes.c_void_p
 
@@ -65,7 +67,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, c
 class Dist(ctypes.Structure):
     """pt_cell_dist (include/pt_cell.h): SyncBN hook and the early-gradient event."""
     _fields_ = [("bn_world", ctypes.c_int32), ("bn_buf", _P), ("allreduce", ALLREDUCE_FN),
-                ("user", _P), ("grads_early_event", _P)]
+                ("user", _P), ("grads_early_event", _P), ("grads_mid_event", _P)]
 
 
 class PtCellError(RuntimeError):
@@ -156,6 +158,8 @@ def _open(path):
         lib.pt_cell_timing_read.restype = ctypes.c_int
         lib.pt_cell_timing_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_int64)]
+        lib.pt_cell_split_bits.restype = ctypes.c_int
+        lib.pt_cell_split_bits.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         lib.pt_cell_trace.restype = ctypes.c_int
         lib.pt_cell_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.pt_cell_timing_reset.restype = ctypes.c_int
@@ -165,10 +169,16 @@ def _open(path):
         return lib
 
 
-def check(rc: int):
+def check(rc: int, lib=None):
+    """Raise on a non-zero status with the error string of ``lib``, the library
+    that returned it (release and diagnostic builds can both be open)."""
     if rc != 0:
-        msg = load().pt_last_error().decode(errors="replace")
+        msg = (lib or load()).pt_last_error().decode(errors="replace")
         raise PtCellError(f"pt_cell error {rc}: {msg}")
+
+
+def check_lib(lib, rc: int):
+    check(rc, lib)
 
 
 def timing_read(kind: int):
@@ -176,5 +186,5 @@ def timing_read(kind: int):
     lib = load()
     ms = ctypes.c_double()
     n = ctypes.c_int64()
-    check(lib.pt_cell_timing_read(kind, ctypes.byref(ms), ctypes.byref(n)))
+    check_lib(lib, lib.pt_cell_timing_read(kind, ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value

@@ -152,7 +152,7 @@ class RecurrentCellFn(torch.autograd.Function):
         saved = torch.empty(lib.pt_cell_saved_bytes(ctypes.byref(d)), dtype=torch.uint8,
                             device=x.device)
         if saved.numel() == 0:
-            _lib.check(1)
+            _lib.check(1, lib)
         ws = torch.empty(lib.pt_cell_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                          device=x.device)
         b, t, h, w = clip_dims(x)
@@ -163,14 +163,14 @@ class RecurrentCellFn(torch.autograd.Function):
         st = _stream(x.device)
         dd = (cdist.struct(lib.pt_cell_bn_sync_doubles(ctypes.byref(d)), x.device)
               if cdist is not None else None)
-        _lib.check(lib.pt_cell_forward_dist(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
+        _lib.check_lib(lib, lib.pt_cell_forward_dist(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
                                             _ptr(saved), _ptr(ws), _ptr(e_last),
                                             _ptr(gates) if want_seq else None,
                                             ctypes.byref(dd) if dd is not None else None, st))
         e_seq = torch.empty((b, t, c, h, w) if want_seq else (0,), dtype=torch.float32,
                             device=x.device)
         if want_seq:
-            _lib.check(lib.pt_cell_export_exc(ctypes.byref(d), _ptr(saved), _ptr(e_seq), st))
+            _lib.check_lib(lib, lib.pt_cell_export_exc(ctypes.byref(d), _ptr(saved), _ptr(e_seq), st))
         ctx.cfg = cfg
         ctx.cdist = cdist
         ctx.lib = lib                      # the backward runs on the library that wrote `saved`
@@ -201,15 +201,19 @@ class RecurrentCellFn(torch.autograd.Function):
         pp = _pack(_lib.Params, params)
         gg = _pack(_lib.Grads, grads)
         cdist = ctx.cdist
-        early = None
+        early = mid = None
         bucket = cdist.bucket if cdist is not None else None
         if bucket is not None and cdist.world() > 1:
             early = torch.cuda.Event()
             early.record()                  # creates the event; the library re-records it
+            if not ctx.cfg.no_inh and bucket.three_part:
+                mid = torch.cuda.Event()
+                mid.record()
         dd = (cdist.struct(lib.pt_cell_bn_sync_doubles(ctypes.byref(d)), x.device,
-                           early.cuda_event if early is not None else None)
+                           early.cuda_event if early is not None else None,
+                           mid.cuda_event if mid is not None else None)
               if cdist is not None else None)
-        _lib.check(lib.pt_cell_backward_dist(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
+        _lib.check_lib(lib, lib.pt_cell_backward_dist(ctypes.byref(d), _ptr(x), ctypes.byref(pp),
                                              _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_e_last),
                                              ctypes.byref(gg),
                                              ctypes.byref(dd) if dd is not None else None,
@@ -217,9 +221,13 @@ class RecurrentCellFn(torch.autograd.Function):
         if early is not None:
             # every gradient but the two k x k weights is final at `early`:
             # averaged on a side stream under the k x k weight-gradient kernel
-            from .dist import LATE_KEYS
+            from .dist import LATE_KEYS, MID_KEYS
             bucket.reduce_early([(pid, g) for k, pid, g in zip(PARAM_KEYS, ctx.param_ids, grads)
                                  if g is not None and k not in LATE_KEYS], early)
+            if mid is not None:
+                # w_inh is final at `mid`: averaged under w_exc's weight-gradient launch
+                bucket.reduce_early([(pid, g) for k, pid, g in zip(PARAM_KEYS, ctx.param_ids, grads)
+                                     if g is not None and k in MID_KEYS], mid)
         ctx.saved_blob = None
         return (None, None, None, None, *grads)
 

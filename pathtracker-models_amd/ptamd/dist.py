@@ -16,9 +16,13 @@ include/pt_cell.h), configured through :class:`CellDist`:
   together compute exactly the single-process batch (4 T small all-reduces per
   step, host callbacks between launches, no hipGraph replay);
 * gradient overlap: the cell's gradients other than the two k x k weights are
-  final before the k x k weight-gradient kernel (~2.5 ms at the headline
+  final before the k x k weight-gradient kernel (~2.1 ms at the headline
   size) starts; :class:`GradBucket` averages them on a side stream while that
-  kernel runs, and only the k x k weights (and the readout) afterwards.
+  kernel runs.  With the r06 three-part exchange the kernel runs as two
+  launches, w_inh's first: w_inh's gradient (50,176 floats) is averaged on the
+  side stream while w_exc's launch runs, so 56,896 of the 107,190 floats
+  (53 %) are exchanged under the backward; only w_exc and the readout are
+  averaged afterwards.
 """
 from __future__ import annotations
 
@@ -30,6 +34,9 @@ import torch.distributed as dist
 
 # cell gradients final before the k x k weight-gradient kernel (ptamd.cell.PARAM_KEYS)
 LATE_KEYS = ("unit1.w_exc", "unit1.w_inh")
+# (r06) the k x k weight final between its own weight-gradient launch and
+# w_exc's (pt_cell_dist.grads_mid_event): averaged under w_exc's launch
+MID_KEYS = ("unit1.w_inh",)
 
 
 def env_rank():
@@ -46,8 +53,9 @@ class GradBucket:
     (plus, with a :class:`CellDist` overlap, one earlier side-stream all-reduce
     of the cell's early gradients)."""
 
-    def __init__(self, params, device, group=None):
+    def __init__(self, params, device, group=None, three_part=True):
         self.params = [p for p in params if p.requires_grad]
+        self.three_part = three_part    # w_inh averaged under w_exc's weight-gradient launch
         self.numel = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.group = group
@@ -62,6 +70,16 @@ class GradBucket:
         therefore overlaps.  Called from the cell's autograd backward."""
         world = _world(self.group)
         if world == 1 or not pairs:
+            return
+        if not pairs[0][1].is_cuda:       # CPU ranks (gloo): the same exchange, in order
+            flat = torch.cat([g.reshape(-1) for _, g in pairs])
+            dist.all_reduce(flat, group=self.group)
+            flat.mul_(1.0 / world)
+            off = 0
+            for _, g in pairs:
+                g.copy_(flat[off:off + g.numel()].view_as(g))
+                off += g.numel()
+            self._early_done |= {pid for pid, _ in pairs}
             return
         main = torch.cuda.current_stream()
         if self._side is None:
@@ -79,7 +97,7 @@ class GradBucket:
                 g.record_stream(side)
                 off += n
         main.wait_stream(side)
-        self._early_done = {pid for pid, _ in pairs}
+        self._early_done |= {pid for pid, _ in pairs}       # (early, then mid: both this step)
 
     def allreduce_mean(self):
         world = _world(self.group)
@@ -147,7 +165,7 @@ class CellDist:
             traceback.print_exc()
             return 1
 
-    def struct(self, bn_doubles, device, early_event=None):
+    def struct(self, bn_doubles, device, early_event=None, mid_event=None):
         """The pt_cell_dist for one call (``bn_doubles`` = pt_cell_bn_sync_doubles)."""
         from . import _lib
         d = _lib.Dist()
@@ -158,6 +176,7 @@ class CellDist:
             d.allreduce = self._cfn
         d.user = None
         d.grads_early_event = early_event
+        d.grads_mid_event = mid_event
         return d
 
 

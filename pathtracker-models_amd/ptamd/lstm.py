@@ -137,10 +137,17 @@ def _open(path):
         return lib
 
 
-def check(rc: int):
+def check(rc: int, lib=None):
+    """Raise on a non-zero status; the message comes from ``lib``, the library
+    that returned it (its error string is per library: the release and the
+    diagnostic builds can both be open, ptamd.lstm.diag_library)."""
     if rc != 0:
-        msg = load().pt_lstm_last_error().decode(errors="replace")
+        msg = (lib or load()).pt_lstm_last_error().decode(errors="replace")
         raise PtLstmError(f"pt_lstm error {rc}: {msg}")
+
+
+def _chk(lib, rc: int):
+    check(rc, lib)
 
 
 DTYPES = {"f32": PT_LSTM_F32, "fp32": PT_LSTM_F32, "float32": PT_LSTM_F32,
@@ -202,7 +209,7 @@ class LSTMStepsFn(torch.autograd.Function):
         d = make_desc(x, ch, ksize, steps, dtype, h0, c0)
         nsaved = lib.pt_lstm_saved_bytes(ctypes.byref(d))
         if nsaved == 0:
-            check(1)
+            check(1, lib)
         saved = torch.empty(nsaved, dtype=torch.uint8, device=x.device)
         b, hh, ww = x.shape[0], x.shape[-2], x.shape[-1]
         h_out = torch.empty((b, ch, hh, ww), dtype=torch.float32, device=x.device)
@@ -213,19 +220,20 @@ class LSTMStepsFn(torch.autograd.Function):
             pp.bx[g] = weights[4 + g].data_ptr()
             pp.wh[g] = weights[8 + g].data_ptr()
         st = _stream(x.device)
-        check(lib.pt_lstm_forward(ctypes.byref(d), _ptr(x), ctypes.byref(pp), _ptr(h0), _ptr(c0),
+        _chk(lib, lib.pt_lstm_forward(ctypes.byref(d), _ptr(x), ctypes.byref(pp), _ptr(h0), _ptr(c0),
                                   _ptr(saved), _ptr(h_out), _ptr(c_out), st))
         jv = torch.empty((0,), device=x.device)
         if want_jv:
             ws = torch.empty(lib.pt_lstm_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                              device=x.device)
             jv = torch.empty_like(h_out)
-            check(lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
+            _chk(lib, lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
                                          _ptr(jv), st))
         h_seq = torch.empty((b, ch, steps, hh, ww) if want_seq else (0,), device=x.device)
         if want_seq:
-            check(lib.pt_lstm_export_h(ctypes.byref(d), _ptr(saved), _ptr(h_seq), st))
+            _chk(lib, lib.pt_lstm_export_h(ctypes.byref(d), _ptr(saved), _ptr(h_seq), st))
         ctx.meta = (ksize, steps, dtype, h0 is not None, c0 is not None, tuple(x.shape), ch)
+        ctx.lib = lib
         ctx.desc = d
         ctx.saved_blob = saved
         ctx.wshapes = [w.shape for w in weights]
@@ -237,8 +245,9 @@ class LSTMStepsFn(torch.autograd.Function):
     def backward(ctx, d_h, d_c, _d_jv, _d_seq):
         # may run several times on one graph (retain_graph: the rbp Neumann
         # series and the Jacobian-penalty VJPs, models/convlstm.py:35,155-160),
-        # so the saved blob stays with ctx until autograd frees the graph
-        lib = load()
+        # so the saved blob stays with ctx until autograd frees the graph; the
+        # library that wrote it runs the backward
+        lib = ctx.lib
         ksize, steps, dtype, has_h0, has_c0, xshape, ch = ctx.meta
         b, hh, ww = xshape[0], xshape[-2], xshape[-1]
         dev = ctx.saved_blob.device
@@ -263,7 +272,7 @@ class LSTMStepsFn(torch.autograd.Function):
         gg.d_x = dx.data_ptr() if dx is not None else 0
         gg.d_h0 = dh0.data_ptr() if dh0 is not None else 0
         gg.d_c0 = dc0.data_ptr() if dc0 is not None else 0
-        check(lib.pt_lstm_backward(ctypes.byref(d), _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_h),
+        _chk(lib, lib.pt_lstm_backward(ctypes.byref(d), _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_h),
                                    _ptr(d_c), ctypes.byref(gg), _stream(dev)))
         return (dx, dh0, dc0, None, None, None, None, None, None, *grads)
 
@@ -311,7 +320,7 @@ class StemStepsFn(torch.autograd.Function):
                  dtype=DTYPES[dtype], init_state=0, x_seq=1)
         nsaved = lib.pt_lstm_saved_bytes(ctypes.byref(d))
         if nsaved == 0:
-            check(1)
+            check(1, lib)
         saved = torch.empty(nsaved, dtype=torch.uint8, device=x.device)
         h_out = torch.empty((b, ch, hh, ww), dtype=torch.float32, device=x.device)
         c_out = torch.empty_like(h_out)
@@ -321,18 +330,18 @@ class StemStepsFn(torch.autograd.Function):
             pp.bx[g] = weights[4 + g].data_ptr()
             pp.wh[g] = weights[8 + g].data_ptr()
         st = _stream(x.device)
-        check(lib.pt_lstm_forward_stem(ctypes.byref(d), _ptr(x), int(u8), cin_s, _ptr(w), _ptr(bb),
+        _chk(lib, lib.pt_lstm_forward_stem(ctypes.byref(d), _ptr(x), int(u8), cin_s, _ptr(w), _ptr(bb),
                                        ctypes.byref(pp), _ptr(saved), _ptr(h_out), _ptr(c_out), st))
         jv = torch.empty((0,), device=x.device)
         if want_jv:
             ws = torch.empty(lib.pt_lstm_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                              device=x.device)
             jv = torch.empty_like(h_out)
-            check(lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
+            _chk(lib, lib.pt_lstm_jv_penalty(ctypes.byref(d), _ptr(saved), _ptr(ws), float(mu),
                                          _ptr(jv), st))
         h_seq = torch.empty((b, ch, steps, hh, ww) if want_seq else (0,), device=x.device)
         if want_seq:
-            check(lib.pt_lstm_export_h(ctypes.byref(d), _ptr(saved), _ptr(h_seq), st))
+            _chk(lib, lib.pt_lstm_export_h(ctypes.byref(d), _ptr(saved), _ptr(h_seq), st))
         ctx.lib = lib
         ctx.desc = d
         ctx.saved_blob = saved
@@ -366,7 +375,7 @@ class StemStepsFn(torch.autograd.Function):
             gg.bx[g] = grads[4 + g].data_ptr() if grads[4 + g] is not None else 0
             gg.wh[g] = grads[8 + g].data_ptr() if grads[8 + g] is not None else 0
         gg.d_x = gg.d_h0 = gg.d_c0 = 0
-        check(lib.pt_lstm_backward_stem(ctypes.byref(d), _ptr(x), u8, cin_s, _ptr(w), _ptr(bb),
+        _chk(lib, lib.pt_lstm_backward_stem(ctypes.byref(d), _ptr(x), u8, cin_s, _ptr(w), _ptr(bb),
                                         _ptr(ctx.saved_blob), _ptr(ws), _ptr(d_h), _ptr(d_c),
                                         ctypes.byref(gg), _ptr(dsw), _ptr(dsb), _stream(dev)))
         return (None, dsw, dsb, None, None, None, None, None, *grads)
@@ -408,9 +417,10 @@ class StemFn(torch.autograd.Function):
         w = weight.detach().reshape(cout, cin).contiguous().float()
         bb = bias.detach().contiguous().float()
         y = torch.empty((b, cout) + dims, device=x.device)
-        check(lib.pt_lstm_stem_forward(_ptr(x), int(u8), _ptr(w), _ptr(bb), b, cin, cout, n,
+        _chk(lib, lib.pt_lstm_stem_forward(_ptr(x), int(u8), _ptr(w), _ptr(bb), b, cin, cout, n,
                                        _ptr(y), _stream(x.device)))
         ctx.save_for_backward(x, w, bb)
+        ctx.lib = lib
         ctx.meta = (int(u8), b, cin, n)
         ctx.wshape = weight.shape
         return y
@@ -418,7 +428,7 @@ class StemFn(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, dy):
-        lib = load()
+        lib = ctx.lib
         x, w, bb = ctx.saved_tensors
         u8, b, cin, n = ctx.meta
         cout = w.shape[0]
@@ -426,7 +436,7 @@ class StemFn(torch.autograd.Function):
         ws = torch.empty(lib.pt_lstm_stem_workspace_bytes(cin), dtype=torch.uint8, device=x.device)
         dw = torch.empty((cout, cin), device=x.device)
         db = torch.empty((cout,), device=x.device)
-        check(lib.pt_lstm_stem_backward(_ptr(x), u8, _ptr(w), _ptr(bb), _ptr(dy), b, cin, cout,
+        _chk(lib, lib.pt_lstm_stem_backward(_ptr(x), u8, _ptr(w), _ptr(bb), _ptr(dy), b, cin, cout,
                                         n, _ptr(ws), _ptr(dw), _ptr(db), _stream(x.device)))
         return None, dw.reshape(ctx.wshape), db
 

@@ -81,14 +81,15 @@ class ReadoutFn(torch.autograd.Function):
         logits = torch.empty(b, device=e.device, dtype=torch.float32)
         pooled = torch.empty(b, device=e.device, dtype=torch.float32)
         pp = _params(ws)
-        _lib.check(lib.pt_readout_forward(ctypes.byref(d), _ptr(e), _ptr(tgt), ctypes.byref(pp),
+        _lib.check_lib(lib, lib.pt_readout_forward(ctypes.byref(d), _ptr(e), _ptr(tgt), ctypes.byref(pp),
                                           _ptr(logits), _ptr(pooled), _stream(e.device)))
         ctx.save_for_backward(e, tgt, pooled, *ws)
+        ctx.lib = lib                       # the backward runs in the same library
         return logits.reshape(b, 1)
 
     @staticmethod
     def backward(ctx, d_logits):
-        lib = load()
+        lib = ctx.lib
         e, tgt, pooled, *ws = ctx.saved_tensors
         b, c, h, w = e.shape
         d = RoDesc(b, c, h, w)
@@ -99,7 +100,7 @@ class ReadoutFn(torch.autograd.Function):
                               dtype=torch.uint8, device=e.device)
         pp = _params(ws)
         gg = RoGrads(*[_ptr(g) for g in grads])
-        _lib.check(lib.pt_readout_backward(ctypes.byref(d), _ptr(e), _ptr(tgt), ctypes.byref(pp),
+        _lib.check_lib(lib, lib.pt_readout_backward(ctypes.byref(d), _ptr(e), _ptr(tgt), ctypes.byref(pp),
                                            _ptr(pooled), _ptr(dl), _ptr(d_e), ctypes.byref(gg),
                                            _ptr(scratch), _stream(e.device)))
         need = ctx.needs_input_grad

@@ -35,7 +35,7 @@ def _shard_grads(sd, x, y):
     return leaf
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, port, out_q, parts=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -51,7 +51,16 @@ def _worker(rank, world, port, out_q):
     shard = slice(rank * 2, rank * 2 + 2)
     leaf = _shard_grads(sd, x[shard], y[shard])
     bucket = GradBucket(list(leaf.values()), "cpu")
+    if parts == 3:
+        # the three-part exchange in the cell backward's order (ptamd.cell):
+        # the early cell gradients, then w_inh, then allreduce_mean the rest
+        from ptamd.dist import LATE_KEYS, MID_KEYS
+        cell = [k for k in leaf if k.startswith("unit1.") and leaf[k].grad is not None]
+        bucket.reduce_early([(id(leaf[k]), leaf[k].grad) for k in cell if k not in LATE_KEYS], None)
+        bucket.reduce_early([(id(leaf[k]), leaf[k].grad) for k in cell if k in MID_KEYS], None)
+        assert len(bucket._early_done) == len(cell) - 1
     bucket.allreduce_mean()
+    assert not bucket._early_done
     opt = torch.optim.Adam([v for v in leaf.values() if v.requires_grad], lr=3e-4)
     opt.step()
     # numpy (pickled by value): torch tensors would travel as fds of a dead process
@@ -62,11 +71,14 @@ def _worker(rank, world, port, out_q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gradient_average_and_identical_params():
+@pytest.mark.parametrize("parts", [1, 3])
+def test_two_rank_gradient_average_and_identical_params(parts):
+    """parts=1: one flat bucket after backward; parts=3: r06's three-part
+    exchange (early cell gradients, w_inh, the rest)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, parts)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (gr, pr)) for r, gr, pr in (q.get(timeout=240) for _ in range(2)))

@@ -14,8 +14,10 @@ ptamd.dist.CellDist, against the single-process HIP cell.
 * early-gradient overlap: with per-replica BatchNorm (the default) the
   gradients averaged in two parts -- the cell's early gradients on a side
   stream behind the event the backward records before its k x k
-  weight-gradient kernel, the rest after backward -- equal the mean of the
-  per-shard single-process gradients.
+  weight-gradient kernel, the rest after backward -- or in three (r06: w_inh
+  on the side stream behind the event recorded between w_inh's and w_exc's
+  weight-gradient launches) equal the mean of the per-shard single-process
+  gradients.
 """
 import os
 import socket
@@ -57,7 +59,7 @@ def _batch():
     return x, torch.tensor([ord(v) for v in labels], dtype=torch.float32)
 
 
-def _worker(rank, world, port, sync_bn, out_q, dtype="f32"):
+def _worker(rank, world, port, sync_bn, out_q, dtype="f32", three_part=True):
     import sys
     sys.path[:0] = [os.path.join(REPO, "tests"), REPO, os.path.join(REPO, "pathtracker-models_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -70,7 +72,7 @@ def _worker(rank, world, port, sync_bn, out_q, dtype="f32"):
     m.cell_dtype = dtype
     x, y = _batch()
     sh = slice(2 * rank, 2 * rank + 2)
-    bucket = GradBucket(m.parameters(), dev)
+    bucket = GradBucket(m.parameters(), dev, three_part=three_part)
     m.cell_dist = CellDist(sync_bn=sync_bn, bucket=bucket)
     out, _ = m(x[sh].to(dev))
     F.binary_cross_entropy_with_logits(out, y[sh].to(dev).reshape(-1, 1)).backward()
@@ -84,12 +86,12 @@ def _worker(rank, world, port, sync_bn, out_q, dtype="f32"):
     dist.destroy_process_group()
 
 
-def _run_ranks(sync_bn, dtype="f32"):
+def _run_ranks(sync_bn, dtype="f32", three_part=True):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, sync_bn, q, dtype)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sync_bn, q, dtype, three_part)) for r in range(2)]
     for p in procs:
         p.start()
     res = {r: rest for r, *rest in (q.get(timeout=200) for _ in range(2))}
@@ -151,15 +153,19 @@ def test_syncbn_two_ranks_equal_single_process(dtype, atol, rel, min_cos):
 
 
 @pytest.mark.timeout(300)
-def test_early_gradient_overlap_matches_shard_mean():
+@pytest.mark.parametrize("three_part", [True, False])
+def test_early_gradient_overlap_matches_shard_mean(three_part):
+    """Two-part (early cell gradients, then the rest) and r06's three-part
+    exchange (early, w_inh under w_exc's weight-gradient launch, the rest)."""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
-    res = _run_ranks(sync_bn=False)
+    res = _run_ranks(sync_bn=False, three_part=three_part)
     x, y = _batch()
     parts = [_single(x[s], y[s]) for s in (slice(0, 2), slice(2, 4))]
     mean = {k: (parts[0][1][k] + parts[1][1][k]) / 2 for k in parts[0][1]}
     for r in (0, 1):
         logits, early, grads = res[r]
         torch.testing.assert_close(torch.from_numpy(logits), parts[r][0], rtol=0, atol=1e-6)
-        assert early == 22                               # every cell param but w_exc / w_inh
+        # every cell param but w_exc / w_inh, and w_inh too in the three-part form
+        assert early == (23 if three_part else 22)
         _close_grads(grads, mean, 1e-5)

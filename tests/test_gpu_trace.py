@@ -93,19 +93,25 @@ lib = _lib.load()
 assert "diag" in lib.pt_version().decode()
 o0, g0 = run()
 dev = torch.device("cuda:0")
-buf = torch.zeros(_lib.NKINDS * 256 * 16, dtype=torch.int64, device=dev)
+buf = torch.zeros(_lib.NKINDS * _lib.TRACE_WG * _lib.TRACE_SLOTS, dtype=torch.int64, device=dev)
 assert lib.pt_cell_trace(ctypes.c_void_p(buf.data_ptr()), 1) == 0
 try:
     o1, g1 = run()
 finally:
     lib.pt_cell_trace(None, -1)
 assert torch.equal(o0, o1) and all(torch.equal(g0[k], g1[k]) for k in g0)
-tr = buf.view(_lib.NKINDS, 256, 16).cpu()
-for kind, slots in (("k_pw_bb", [0, 1, 2, 3, 4, 5, 6]), ("k_pw_ba", [0, 2, 3, 4, 5, 6]),
-                    ("k_fused_fa", [0, 2, 3, 4, 5, 6]), ("k_fused_fb", [0, 2, 3, 4, 5, 6])):
+tr = buf.view(_lib.NKINDS, _lib.TRACE_WG, _lib.TRACE_SLOTS).cpu()
+# (kind, ordered phase slots, per-wave slot base, waves): r06 adds the workgroup's
+# XCC / HW_ID word (slot 7, bit 40 set) and per-wave stamps
+for kind, slots, wbase, nw in (("k_pw_bb", [0, 1, 2, 3, 4, 5, 6], 8, 8), ("k_pw_ba", [0, 2, 3, 4, 5, 6], 8, 4),
+                               ("k_fused_fa", [0, 2, 3, 4, 5, 6], 16, 8),
+                               ("k_fused_fb", [0, 2, 3, 4, 5, 6], 16, 8), ("k_conv_bb", [0, 1, 2], 16, 8)):
     r = tr[_lib.KIND_NAMES.index(kind)]
     live = r[:, 0] > 0
     assert live.any(), kind
+    assert ((r[live][:, 7] >> 40) == 1).all(), kind
+    w = r[live][:, wbase:wbase + nw]
+    assert (w > 0).all() and (w >= r[live][:, slots[0]:slots[0] + 1]).all(), kind
     r = r[live][:, slots]
     assert (r > 0).all(), kind
     assert (r[:, 1:] >= r[:, :-1]).all(), kind            # phases in order per workgroup

@@ -87,6 +87,38 @@ def test_size_queries_and_validation():
     assert b"x_format" in lib.pt_last_error()
 
 
+def test_state_split_round_trips_and_keeps_nan():
+    """The bf16 cell's hi / lo split of E and I (pt_cell_split_bits: the same
+    inline function the kernels' stores use): hi + sext(lo) gives
+    every finite value and +-Inf back bit for bit, hi is the value rounded half
+    up in magnitude, and a NaN stays NaN in hi and in hi + lo (including the
+    mantissas whose half-up add would carry out of the exponent)."""
+    from ptamd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(0)
+    fin = (rng.standard_normal(20000) * 10.0 ** rng.integers(-40, 38, 20000)).astype(np.float32)
+    special = np.array([0.0, -0.0, np.inf, -np.inf, 3.4028235e38, -3.4028235e38, 1e-45, -1e-45,
+                        np.float32(1.0) + np.float32(2 ** -8), np.float32(1.0) + np.float32(2 ** -9)],
+                       dtype=np.float32)
+    nan_bits = np.array([0x7FC00000, 0x7FFF8000, 0x7FFFFFFF, 0xFFFF8000, 0xFFFFFFFF, 0x7F800001,
+                         0x7F808000, 0xFF800001, 0x7FBFFFFF], dtype=np.uint32)
+    bits = np.concatenate([fin.view(np.uint32), special.view(np.uint32), nan_bits])
+    n = len(bits)
+    hi = np.zeros(n, np.uint16)
+    lo = np.zeros(n, np.uint16)
+    assert lib.pt_cell_split_bits(bits.ctypes.data, hi.ctypes.data, lo.ctypes.data, n) == 0
+    back = ((hi.astype(np.uint32) << 16) + lo.astype(np.int16).astype(np.int64).astype(np.uint32)).astype(np.uint32)
+    hif = (hi.astype(np.uint32) << 16).view(np.float32)
+    isn = np.isnan(bits.view(np.float32))
+    assert isn.sum() == len(nan_bits)
+    assert np.array_equal(back[~isn], bits[~isn])
+    assert np.isnan(hif[isn]).all() and np.isnan(back.view(np.float32)[isn]).all()
+    # hi: half up in magnitude (ties away from zero), i.e. the upper 16 bits of bits + 0x8000
+    ref = ((bits[~isn].astype(np.uint64) + 0x8000) >> 16).astype(np.uint16)
+    assert np.array_equal(hi[~isn], ref)
+    assert lib.pt_cell_split_bits(None, None, None, 1) != 0
+
+
 def test_u8_input_helpers_match_prepare_data():
     """The u8 input path's conversion and readout target are bit-identical to
     engine.prepare_data's f32 tensor (utils/engine.py:220-255)."""
