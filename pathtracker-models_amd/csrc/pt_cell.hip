@@ -1238,6 +1238,30 @@ constexpr int CONV_NT = 512;
 // per-column barrier); each finished output row adds its addends and is
 // stored at once (no prefetch: the co-resident workgroup covers the latency).
 // Per output row the MFMA order is that of k_conv_bwd: results bit-identical.
+// Issue priority (r06, the HW_ID trace: profiles/r06_trace_phases.txt).  The
+// SIMD arbiter favours the older wave at equal priority, so the half a kernel
+// starts second runs starved and ends last: the band-1 waves (4-7) of the
+// staggered segments and of k_conv_bwd_band2 -- the critical path of both --
+// and the second workgroup on a CU in k_pw_bb2 / k_pw_ba (rows ending ~10 us
+// after the first one's).  PT_PRIO bit 0: band-1 waves at priority 1 in the
+// fused segments; bit 1: the same in k_conv_bwd_band2; bit 2: the backward
+// point-wise kernels lower their priority as they progress (3 - set / row),
+// so the workgroup that is ahead yields to the one behind; bit 3: and the
+// workgroup dispatched first on a CU (the first half of a 2-per-CU grid:
+// blocks j and j + grid/2 share a CU, the trace shows) one level lower at
+// the same step, so at equal progress the younger one wins, not the older.
+// Default 7 (bits 0-2; bit 3 measured slower: k_pw_bb2 53.7 -> 55.4 us):
+// with RA_FA = 3 the step's device time 21.38 -> 20.64 ms
+// (profiles/r06_libab_prio_{a,b,c}.txt, interleaved in one process).
+#ifndef PT_PRIO
+#define PT_PRIO 7
+#endif
+__device__ __forceinline__ void prio_by_step(int step) {   // 3 - step, clamped; step wave-uniform
+  if (step <= 0) __builtin_amdgcn_s_setprio(3);
+  else if (step == 1) __builtin_amdgcn_s_setprio(2);
+  else if (step == 2) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
 // -------------------------------------------------------------------------
 constexpr int BAND_ROWS = 16, BAND_NT = 256, BAND_TR = BAND_ROWS + 2 * PADMAX;
 constexpr int band_tile_bytes() { return BAND_TR * TILE * C * 2; }
@@ -1457,6 +1481,7 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
   __syncthreads();
   PT_TR(a, a.trace_kind, 2);
   const int wb = wave & 3, band = wave >> 2;
+  if ((PT_PRIO & 2) && band == 1) __builtin_amdgcn_s_setprio(1);   // band 1's fill + conv: the critical path
   if (band == 1) {
     band_fill<BAND2_NT / 2>(a, tbl, tile1, cb, BAND_ROWS, tid - BAND2_NT / 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this wave's tile stores are done
@@ -1498,7 +1523,10 @@ constexpr int PWF_RPP = 1;                         // forward rows per wave
 // prefetch / flush, x staging, LDS clears, reductions) is paid once per 16 rows.
 // k_pw_bb stays at one row per wave: looping its body spills (~46 VGPRs) and
 // doubled its row cost.
-constexpr int PWA_RPP = 4;                         // k_pw_ba rows per wave
+#ifndef PT_PWA_RPP
+#define PT_PWA_RPP 4
+#endif
+constexpr int PWA_RPP = PT_PWA_RPP;                // k_pw_ba rows per wave
 #ifndef PT_PWB_RPP
 #define PT_PWB_RPP 1
 #endif
@@ -2104,8 +2132,11 @@ __device__ __forceinline__ void stag_wait(const int* cnt, int wave) {
 #ifndef PT_PERSIST_STAG
 #define PT_PERSIST_STAG 1
 #endif
+// r06: 3 (band 0 three rows per wave, band 1 five) with the band-1 waves at
+// issue priority 1 (PT_PRIO bit 0): k_fused_fa 64.8 -> 62.0 us; 4 / 4 with
+// the priority 66.6, 2 / 6 65.3, 5 / 3 67.6 (profiles/r06_libab_prio_*.txt)
 #ifndef PT_FUSED_STAG_RA_FA
-#define PT_FUSED_STAG_RA_FA 4
+#define PT_FUSED_STAG_RA_FA 3
 #endif
 #ifndef PT_FUSED_STAG_RA_FB
 #define PT_FUSED_STAG_RA_FB 3
@@ -2146,6 +2177,7 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
     __syncthreads();
     PT_TR(a, PT_K_FUSED_FA, 2);
     const int nr = stag_rows<PT_FUSED_STAG_RA_FA>(wave);
+    if ((PT_PRIO & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);   // band 1: the critical path
 #pragma unroll 1
     for (int i = 0; i < nr; ++i) {
       const int y = stag_row<PT_FUSED_STAG_RA_FA>(wave, i);
@@ -2209,6 +2241,7 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     __syncthreads();
     PT_TR(a, PT_K_FUSED_FB, 2);
     const int nr = stag_rows<PT_FUSED_STAG_RA_FB>(wave);
+    if ((PT_PRIO & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);   // band 1: the critical path
 #pragma unroll 1
     for (int i = 0; i < nr; ++i) {
       const int y = stag_row<PT_FUSED_STAG_RA_FB>(wave, i);
@@ -2349,6 +2382,8 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
 
 #pragma unroll 1
   for (int i = 0; i < RPP && !(PT_ABL(a.ablate) & 4); ++i) {
+    if constexpr ((PT_PRIO & 4) != 0)
+      prio_by_step(i + ((PT_PRIO & 8) && blockIdx.x < gridDim.x / 2 ? 1 : 0));
     const int yl = wave * RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
     f32x16 GE;
@@ -2845,6 +2880,8 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_bb2(CellArgs<S> a) {
   // set's element-wise temporaries are dead, before its barriers
   Pb2In<S> in1;
   auto set_body = [&](const int set, const Pb2In<S> in) {
+    if constexpr ((PT_PRIO & 4) != 0)
+      prio_by_step(set + ((PT_PRIO & 8) && blockIdx.x < gridDim.x / 2 ? 1 : 0));
     // the lane index laundered per set: the per-lane parameters and addresses
     // are formed in the set instead of living across both as invariants
     int tl = tid;

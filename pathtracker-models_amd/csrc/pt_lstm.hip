@@ -1039,13 +1039,16 @@ __global__ void k_lreduce(LReduceArgs r) {
 // ------------------------------------------------------------ conversions
 // NCHW fp32 [B][nc][NPIX] -> channels-last [B][NPIX][32] (zero padded).
 // tn > 1: frame t of [B][nc][tn][NPIX] (x_seq inputs / their gradients).
+// lo (optional): the residual v - (S)v as a second plane (the split x-conv)
 template <class S>
 __global__ void k_to_cl(const float* __restrict__ src, S* __restrict__ dst, int B, int nc,
-                        int tn = 1, int t = 0) {
+                        int tn = 1, int t = 0, S* __restrict__ lo = nullptr) {
   const int n = B * NPIX * HC;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const int c = e % HC, pix = (e / HC) % NPIX, b = e / (HC * NPIX);
-    dst[e] = (S)(c < nc ? src[(((size_t)b * nc + c) * tn + t) * NPIX + pix] : 0.f);
+    const float v = c < nc ? src[(((size_t)b * nc + c) * tn + t) * NPIX + pix] : 0.f;
+    dst[e] = (S)v;
+    if (lo) lo[e] = (S)(v - (float)(S)v);
   }
 }
 // All steps at once: [B][nc][T][NPIX] fp32 <-> [T][B][NPIX][32] channels-last
@@ -1131,16 +1134,18 @@ struct LPrepArgs {
   const float* bx[4];
   void* fr[4];
   float* bias;     // [128]
+  void* frlo;      // or null: family 4, Wx fwd's residual W - (S)W (the split x-conv)
 };
 template <class S>
 __global__ void k_lprep(LPrepArgs p) {
   using TT = Tr<S>;
   const int KK = p.K * p.K;
   const int per = NG * KK * TT::KS * 64 * TT::EPL;     // elements per family
-  const int total = 4 * per + GC;
+  const int nfam = p.frlo ? 5 : 4;
+  const int total = nfam * per + GC;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-    if (e >= 4 * per) {
-      const int c = e - 4 * per, g = c / 32, co = c % 32;
+    if (e >= nfam * per) {
+      const int c = e - nfam * per, g = c / 32, co = c % 32;
       p.bias[c] = (p.bx[g] && co < p.ch) ? p.bx[g][co] : 0.f;
       continue;
     }
@@ -1149,16 +1154,17 @@ __global__ void k_lprep(LPrepArgs p) {
     const int tap = (r / (TT::EPL * 64 * TT::KS)) % KK, blk = r / (TT::EPL * 64 * TT::KS * KK);
     const int n = l & 31, hh = l >> 5, kc = frag_chan<S>(ks, hh, j);
     float v = 0.f;
-    if (fam < 2) {                      // blk = output gate o
-      const float* W = fam == 0 ? p.wx[blk] : p.wh[blk];
-      const int cin = fam == 0 ? p.cin : p.ch;
+    if (fam < 2 || fam == 4) {          // blk = output gate o
+      const float* W = fam != 1 ? p.wx[blk] : p.wh[blk];
+      const int cin = fam != 1 ? p.cin : p.ch;
       if (n < p.ch && kc < cin) v = W[((size_t)n * cin + kc) * KK + tap];
+      if (fam == 4) v -= (float)(S)v;
     } else {                            // blk = input gate ig; out channel n = fwd input channel
       const float* W = fam == 2 ? p.wh[blk] : p.wx[blk];
       const int cin = fam == 2 ? p.ch : p.cin;
       if (kc < p.ch && n < cin) v = W[((size_t)kc * cin + n) * KK + (KK - 1 - tap)];
     }
-    ((S*)p.fr[fam])[r] = (S)v;
+    ((S*)(fam == 4 ? p.frlo : p.fr[fam]))[r] = (S)v;
   }
 }
 
@@ -1433,6 +1439,8 @@ struct LPlan {
   size_t es, npix;
   // saved
   size_t o_fr[4], o_bias, o_x, o_xg, o_h0, o_c0, o_P, o_h, o_c, saved;
+  size_t o_frlo, o_xlo;   // bf16 static x: the split x-conv's residual fragments / x plane
+  int xsplit;
   // workspace
   size_t o_dh, o_dc, o_dP, o_dPsum, o_dPsumS, o_jvP, o_wsh, o_wsx, o_col, o_dx, o_stem, ws;
 };
@@ -1474,6 +1482,14 @@ LPlan plan(const pt_lstm_desc* d) {
   // static x with a given h0: xg = Wx*x + b kept apart from P_0 (per-step
   // input: P_t = Wx*x_t + b is written into P directly, no xg)
   p.o_xg = o; o += p.xseq ? 0 : al(p.npix * GC * 4);
+  // bf16 static x (r06): xg in three bf16 passes, x_hi W_hi + x_lo W_hi +
+  // x_hi W_lo (~2^-16 relative, f32 accumulation): with bf16 x and Wx the
+  // Gabor-squared input's x-conv pushed tanh(P_c) into saturation with a
+  // bf16-sized error and the c-gate gradients to cosine 0.96
+  // (tools/lstm_bf16_attrib.py, profiles/r06_lstm_bf16_attrib.json)
+  p.xsplit = p.es == 2 && !p.xseq;
+  p.o_frlo = o; o += p.xsplit ? al(NG * KK * 1024 * p.es) : 0;
+  p.o_xlo = o; o += p.xsplit ? al(p.npix * HC * p.es) : 0;
   p.o_h0 = o; o += al(p.npix * HC * p.es);
   p.o_c0 = o; o += al(p.npix * HC * 4);
   p.o_P = o; o += al(p.npix * GC * 4 * p.T);
@@ -1665,6 +1681,7 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   }
   for (int i = 0; i < 4; ++i) pa.fr[i] = sv + p.o_fr[i];
   pa.bias = (float*)(sv + p.o_bias);
+  pa.frlo = p.xsplit ? sv + p.o_frlo : nullptr;
   hipLaunchKernelGGL(k_lprep<S>, dim3(1024), dim3(256), 0, st, pa);
   HIPCHK(hipGetLastError());
 
@@ -1679,7 +1696,8 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
     hipLaunchKernelGGL(k_to_cl_seq<S>, dim3(p.B * p.T * (NPIX / SEQ_CH)), dim3(256), 0, st, x, xcl,
                        p.B, p.cin, p.T);
   else
-    hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, x, xcl, p.B, p.cin);
+    hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, x, xcl, p.B, p.cin, 1, 0,
+                       p.xsplit ? (S*)(sv + p.o_xlo) : nullptr);
   S* hinit = h0 ? (S*)(sv + p.o_h0) : nullptr;
   float* cinit = c0 ? (float*)(sv + p.o_c0) : nullptr;
   if (h0) hipLaunchKernelGGL(k_to_cl<S>, grid_for(p.npix * HC), dim3(256), 0, st, h0, hinit, p.B, p.ch);
@@ -1704,6 +1722,10 @@ int run_forward(const pt_lstm_desc* d, const float* x, const pt_lstm_params* pr,
   if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_fr[0], p.xseq ? P : xg, nullptr, pa.bias,
                                dual ? p.B : p.xseq ? p.B * p.T : p.B, st))
     return rc;
+  if (p.xsplit) {        // xg += Wx_hi x_lo + Wx_lo x_hi (in place: out = acc + add, per thread)
+    if (int rc = conv_k<S, 1, 4>(p.K, sv + p.o_xlo, sv + p.o_fr[0], xg, xg, nullptr, p.B, st)) return rc;
+    if (int rc = conv_k<S, 1, 4>(p.K, xcl, sv + p.o_frlo, xg, xg, nullptr, p.B, st)) return rc;
+  }
   for (int t = 0; t < p.T; ++t) {
     const S* hin = t == 0 ? hinit : H + (t - 1) * hstep;
     if (dual && t > 0) {     // (r05) + the step's point-wise update in the conv's epilogue

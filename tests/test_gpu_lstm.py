@@ -111,9 +111,11 @@ def test_convlstm_jacobian_penalty_bf16_vs_f32():
     """jacobian_penalty=True with the bf16 cell: the library's first T-2 steps
     store bf16 states, which feed the last two steps' f32 torch ops and their
     double backward.  Against the f32 run (itself pinned to the reference
-    golden above): the penalty within 5 % relative RMS, the output within 3 %
-    (bf16 tolerance of test_convlstm_bf16_tolerance), gradient cosine > 0.95
-    per tensor; measured values recorded (gpurun_out/parity_records.json)."""
+    golden above): the penalty within 5 % relative RMS, the output within 1 %,
+    gradient cosine > 0.999 per tensor (r06: the static x-conv in three bf16
+    passes, see test_convlstm_bf16_tolerance; r05 measured 0.966 with the
+    single-pass bf16 x-conv and asserted 0.95); measured values recorded
+    (gpurun_out/parity_records.json)."""
     from goldens import record
     from models import convlstm as cl
     dev = _dev()
@@ -140,20 +142,29 @@ def test_convlstm_jacobian_penalty_bf16_vs_f32():
         if g32[k].norm() > 0:
             cos = float(g16[k] @ g32[k] / (g16[k].norm() * g32[k].norm()))
             worst = min(worst, cos)
-            assert cos > 0.95, (k, cos)
     record("convlstm_jvp_bf16_vs_f32", {"penalty_rel_rms": rel(j16, j32), "output_rel_rms": rel(o16, o32),
                                         "min_grad_cos": worst})
+    for k in g32:
+        if g32[k].norm() > 0:
+            cos = float(g16[k] @ g32[k] / (g16[k].norm() * g32[k].norm()))
+            assert cos > 0.999, (k, cos)
     assert rel(j16, j32) < 5e-2, rel(j16, j32)
-    assert rel(o16, o32) < 3e-2, rel(o16, o32)
+    assert rel(o16, o32) < 1e-2, rel(o16, o32)
 
 
 def test_convlstm_bf16_tolerance():
     """bf16 operands / saved h, f32 gate math and accumulation, k=15: outputs
-    (after the batch-statistics BN, which amplifies h's rounding) within 3 %
-    relative RMS of the reference; gradient cosine > 0.95 per tensor.  The
-    weakest tensors are the c-gate's (measured 0.96-0.97): with the Gabor-squared
-    input its pre-activations saturate tanh, where 1 - g^2 is exponentially
-    sensitive to the bf16 rounding of P_c; the other gates measure >= 0.995."""
+    (after the batch-statistics BN, which amplifies h's rounding) within 1 %
+    relative RMS of the reference; gradient cosine > 0.999 per tensor.  Until
+    r05 the static x-conv (xg = Wx x + b, once per forward) ran with bf16 x and
+    Wx: the Gabor-squared input's pre-activations saturate tanh(P_c), where
+    1 - g^2 is exponentially sensitive to P_c's error, and the c-gate
+    gradients measured cosine 0.96-0.97 (asserted 0.95).  The CPU attribution
+    (tools/lstm_bf16_attrib.py, profiles/r06_lstm_bf16_attrib.json) puts all of
+    it on that x-conv's forward value -- x and Wx rounding, not h, dP, Wh or the
+    weight gradient's X operand -- and predicts 0.99999 once that value is
+    near f32; r06 computes it in three bf16 passes (hi x hi + lo x hi + hi x
+    lo).  Measured values recorded (gpurun_out/parity_records.json)."""
     dev = _dev()
     g = load("convlstm_k15")
     m = _model(g, "bf16").to(dev).train()
@@ -164,7 +175,7 @@ def test_convlstm_bf16_tolerance():
     a = out.detach().cpu().double()
     b = torch.from_numpy(g["output"]).double()
     rel = float((a - b).norm() / b.norm())
-    assert rel < 3e-2, f"bf16 output relative RMS error {rel:.3e}"
+    assert rel < 1e-2, f"bf16 output relative RMS error {rel:.3e}"
     cos = {}
     for k, p in m.named_parameters():
         b = torch.from_numpy(g["grad." + k]).double().flatten()
@@ -172,8 +183,11 @@ def test_convlstm_bf16_tolerance():
             continue
         a = p.grad.detach().cpu().double().flatten()
         cos[k] = float(a @ b / (a.norm() * b.norm() + 1e-30))
-    bad = {k: round(v, 4) for k, v in cos.items() if v <= 0.95}
-    assert not bad, f"gradient cosine <= 0.95: {bad} (all: {cos})"
+    from goldens import record
+    record("convlstm_k15_bf16_vs_reference", {"output_rel_rms": rel, "min_grad_cos": min(cos.values()),
+                                              "min_grad_cos_tensor": min(cos, key=cos.get)})
+    bad = {k: round(v, 6) for k, v in cos.items() if v <= 0.999}
+    assert not bad, f"gradient cosine <= 0.999: {bad} (all: {cos})"
 
 
 def _oracle_cell_step(sd, x, h, c, k):

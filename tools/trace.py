@@ -19,6 +19,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from ptamd import _lib  # noqa: E402
+if os.environ.get("TRACE_LIB"):          # a diagnostic A/B build (tools/build_ab.sh ... -DPT_DIAG=1)
+    _lib.DIAG_PATH = os.environ["TRACE_LIB"]
 _lib.use_diag()         # the PT_DIAG build (libptcell_diag.so) honours the switches
 from models import InT  # noqa: E402
 
