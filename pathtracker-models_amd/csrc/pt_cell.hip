@@ -1614,6 +1614,12 @@ __device__ __forceinline__ PLds pcarve_bb(char* smem) {
 // once at the end -- instead of two per-row cross-wave LDS reductions (4
 // barriers a row) into a gacc tile; the slab copy holds only the per-channel
 // block.  f32: pcarve (gacc).
+// PT_PWA_PAIR (r06 A/B): the staged 1x1 weight-gradient operands of TWO
+// row sets in LDS, contracted after every second row: one barrier pair per
+// two rows instead of per row (the workgroup's 4 waves align less often)
+#ifndef PT_PWA_PAIR
+#define PT_PWA_PAIR 0
+#endif
 #ifndef PT_PWA_STAGE
 #define PT_PWA_STAGE 1      // 0: the r04 per-row gacc reductions (A/B builds, tools/libab.py)
 #endif
@@ -1622,7 +1628,8 @@ template <class S>
 constexpr int pwa_lds_bytes() {
   return sizeof(S) == 2 && PT_PWA_STAGE
              ? PW_NW * PWA_RPP * IMG * 16 /*xs*/ + PW_NW * SCR_FLOATS * 4 /*scr*/ + 128 * 4 /*stat*/ +
-                   PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ + 3 * stg_bytes<S, PWA_NPX>() /*stage*/ +
+                   PW_NW * NSMALL * 32 * 4 /*small*/ + 512 * 4 /*red*/ +
+                   (PT_PWA_PAIR ? 6 : 3) * stg_bytes<S, PWA_NPX>() /*stage*/ +
                    NSMALL * 32 * 4 /*slab copy: per-channel block*/
              : pw_lds_bytes<PWA_RPP, true>();
 }
@@ -1633,7 +1640,7 @@ __device__ __forceinline__ PLds pcarve_ba(char* smem) {
     char* p = (char*)(l.red + 512);
     l.stage = (bf16x8*)p;
     l.gacc = nullptr;
-    p += 3 * stg_bytes<S, PWA_NPX>();
+    p += (PT_PWA_PAIR ? 6 : 3) * stg_bytes<S, PWA_NPX>();
     l.slabl = (float*)p - SLAB_G;
   }
   return l;
@@ -2364,9 +2371,6 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
   const int gi = wave >> 1, mt = wave & 1;
   f32x4 wacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   constexpr int SE = stg_bytes<S, PWA_NPX>() / (int)sizeof(S);
-  S* st_dap = (S*)L.stage;
-  S* st_xv = st_dap + SE;
-  S* st_E = st_dap + 2 * SE;
   PT_TR(a, PT_K_PW_BA, 2);
 
   const Stem st{a.wpre[c * 3 + 0], a.wpre[c * 3 + 1], a.wpre[c * 3 + 2], a.bpre[c]};
@@ -2386,6 +2390,9 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
       prio_by_step(i + ((PT_PRIO & 8) && blockIdx.x < gridDim.x / 2 ? 1 : 0));
     const int yl = wave * RPP + i, y = y0 + yl;
     const size_t ro = cb + (size_t)y * IMG * C;
+    S* st_dap = (S*)L.stage + (PT_PWA_PAIR ? (i & 1) * 3 * SE : 0);
+    S* st_xv = st_dap + SE;
+    S* st_E = st_dap + 2 * SE;
     f32x16 GE;
     if (tail) {
       f32x16 z, xv;                          // z: nl'(stem pre-activation)
@@ -2481,9 +2488,12 @@ __device__ __forceinline__ void pw_ba_body(const CellArgs<S>& a, char* smem, int
       store_cl(a.dcE + ro, c, h, rb16(RND_T(a), dcE));
     }
     if constexpr (BF) {
-      if (att_wg) {
-        __syncthreads();                  // the set's 4 rows are staged
-        pr_wgrad_acc<S, PWA_NPX>(st_dap, gi == 0 ? st_xv : st_E, mt, wacc, lane);
+      if (att_wg && (!PT_PWA_PAIR || (i & 1) || i + 1 == RPP)) {
+        __syncthreads();                  // the set's 4 rows are staged (PAIR: two sets)
+        for (int q = PT_PWA_PAIR && (i & 1) ? 1 : 0; q >= 0; --q) {
+          const S* sd = st_dap - q * 3 * SE;
+          pr_wgrad_acc<S, PWA_NPX>(sd, gi == 0 ? sd + SE : sd + 2 * SE, mt, wacc, lane);
+        }
         __syncthreads();                  // before the next set restages
       }
     }
@@ -3163,6 +3173,7 @@ __global__ __launch_bounds__(PB2_NT, 4) void k_pw_ba2(CellArgs<S> a) {
   Pa2In<S> in1;
 
   auto set_body = [&](const int set, const Pa2In<S> in) {
+    if constexpr ((PT_PRIO & 4) != 0) prio_by_step(set);
     int tl = tid;
     if constexpr (NSET > 1) asm volatile("" : "+v"(tl));
     const int lane = tl & 63, n = lane & 15, g4 = lane >> 4;
@@ -4618,7 +4629,10 @@ bool pwb2_env() { return PT_SW("PT_PWB2", 1) != 0; }
 // (B=256 T=64, interleaved): 59.9-60.1 vs 58.4-58.7 us for k_pw_ba, which
 // already ran one round of workgroups (4 rows per wave); k_pw_bb2's gain came
 // from halving the rounds, not from the layout.
-bool pwa2_env() { return PT_SW("PT_PWA2", 0) == 1; }
+#ifndef PT_PWA2_DEF
+#define PT_PWA2_DEF 0     // A/B builds: k_pw_ba2 by default
+#endif
+bool pwa2_env() { return PT_SW("PT_PWA2", PT_PWA2_DEF) == 1; }
 // k_wgrad16 (bf16, k = 7) by default; PT_WG16=0 (diagnostic builds only, read per call) selects the
 // 8-wave k_wgrad.
 bool wg16_env() { return PT_SW("PT_WG16", 1) != 0; }

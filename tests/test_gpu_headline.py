@@ -180,8 +180,15 @@ def test_headline_accuracy_f32_bit_identical_to_oracle():
         rec[f"bf16_flips_{name}"] = int(((lo16 > thr) != (lo32 > thr))[far16].sum())
         rec[f"bf16_in_band_{name}"] = int((~far16).sum())
         # every clip, the in-band ones included
-        rec[f"bf16_flips_all_{name}"] = int(((lo16 > thr) != (lo32 > thr)).sum())
+        flip = (lo16 > thr) != (lo32 > thr)
+        rec[f"bf16_flips_all_{name}"] = int(flip.sum())
         rec[f"bf16_closest_f32_margin_{name}"] = float((lo32 - thr).abs().min())
+        # r06: each in-band flip with its f32 margin and
+        # the bf16 deviation there, both in unscaled logit units
+        rec[f"bf16_flip_detail_{name}"] = [
+            {"clip": int(i), "f32_margin_unscaled": float((lo32[i] - thr).abs() / abs(k / w0)),
+             "bf16_dev_unscaled": float((lo16[i] - lo32[i]).abs() / abs(k / w0))}
+            for i in torch.nonzero(flip).flatten().tolist()]
     _record("headline_accuracy_B256_T64_trained_rescaled", rec)
     assert err <= 1e-3, rec
     for thr in ("train_0.5", "eval_0"):
@@ -191,6 +198,14 @@ def test_headline_accuracy_f32_bit_identical_to_oracle():
         # trained case above has no flip among all 256 clips)
         assert rec[f"f32_flips_{thr}"] == 0 and rec[f"bf16_flips_{thr}"] == 0, rec
         assert 0.25 * B <= rec[f"above_{thr}"] <= 0.75 * B, rec     # straddles the threshold
+        # the in-band flips, bounded (r06; measured 1 per threshold, at f32
+        # margins 1.0e-3 / 1.7e-3 of the rescaled logit = 2.9e-5 / 4.9e-5
+        # unscaled): at most 2 per threshold, and each one a clip whose f32
+        # logit lies within north_star's 1e-3 of the threshold with the bf16
+        # cell's deviation there inside that tolerance too
+        assert rec[f"bf16_flips_all_{thr}"] <= 2, rec
+        for f in rec[f"bf16_flip_detail_{thr}"]:
+            assert f["f32_margin_unscaled"] <= BF16_LOGIT_TOL and f["bf16_dev_unscaled"] <= BF16_LOGIT_TOL, rec
 
 
 def test_f32_matches_oracle_over_64_frames():
