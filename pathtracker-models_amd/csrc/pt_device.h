@@ -551,6 +551,9 @@ __device__ __forceinline__ void tile_fill(S* __restrict__ tile, const S* __restr
 #ifndef PT_CONV_FLAT
 #define PT_CONV_FLAT 1
 #endif
+#ifndef PT_CONV_NOWRELOAD
+#define PT_CONV_NOWRELOAD 0          // timing experiments only (wrong results): column 0's weights for every column
+#endif
 #ifndef PT_BAND_LEAD
 #define PT_BAND_LEAD 5               // banded backward conv: addend loads, tile-row steps ahead (r05: 0 / 3 / 5 = conv_bb 38.9 / 35.8 / 35.5 us)
 #endif
@@ -718,7 +721,7 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
           const int i = tr - kh;
           if (i >= 0 && i < RW) acc[i] = TT::mma(bw[kw % NSET][kh][s], av[st % (PF + 1)][s], acc[i]);
         }
-      if constexpr (NSET == 1 && kw + 1 < K && tr >= RW - 1 && tr - (RW - 1) < K) {
+      if constexpr (NSET == 1 && kw + 1 < K && tr >= RW - 1 && tr - (RW - 1) < K && !PT_CONV_NOWRELOAD) {
         constexpr int kd = tr - (RW - 1);
 #pragma unroll
         for (int s = 0; s < KSP; ++s) bw[0][kd][s] = wf[((kd * K + kw + 1) * TT::KS + s) * 64 + lane];
