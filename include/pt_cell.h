@@ -171,7 +171,8 @@ enum { PT_K_PW_FA = 0, PT_K_CONV_FA = 1, PT_K_PW_FB = 2, PT_K_CONV_FB = 3,
        PT_K_WGRAD = 8, PT_K_PREP = 9, PT_K_REDUCE = 10,
        PT_K_FUSED_FA = 11, PT_K_FUSED_FB = 12,     /* bf16 32x32: point-wise + conv per launch */
        PT_K_PERSIST = 13,                          /* opt-in persistent forward, all frames */
-       PT_K_NKINDS = 14 };
+       PT_K_CONV_PW_BA = 14,                       /* bf16 32x32: k_conv_ba(t) + k_pw_ba(t-1) per launch */
+       PT_K_NKINDS = 15 };
 int pt_cell_timing_enable(uint32_t kind_mask);      /* bit k enables kind k; 0 disables */
 int pt_cell_timing_read(int kind, double* total_ms, int64_t* launches);
 int pt_cell_timing_reset(void);

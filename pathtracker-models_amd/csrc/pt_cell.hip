@@ -1249,7 +1249,10 @@ constexpr int CONV_NT = 512;
 // so the workgroup that is ahead yields to the one behind; bit 3: and the
 // workgroup dispatched first on a CU (the first half of a 2-per-CU grid:
 // blocks j and j + grid/2 share a CU, the trace shows) one level lower at
-// the same step, so at equal progress the younger one wins, not the older.
+// the same step, so at equal progress the younger one wins, not the older;
+// bit 4: in k_fused_fb the band-1 waves drop back to 0 and the band-0 waves
+// rise to 1 once the rows are in (band 0's conv ends last there); bit 5:
+// k_conv_bwd_band2's band-1 waves drop to 0 after their fill.
 // Default 7 (bits 0-2; bit 3 measured slower: k_pw_bb2 53.7 -> 55.4 us):
 // with RA_FA = 3 the step's device time 21.38 -> 20.64 ms
 // (profiles/r06_libab_prio_{a,b,c}.txt, interleaved in one process).
@@ -1314,16 +1317,18 @@ struct AddRowBand {
   }
 };
 
-__global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a) {
+// The band's conv with a row hook (hook(i, acc): output row i finished;
+// k_conv_bwd_band adds the addends and stores, k_conv_pw_ba keeps the row).
+constexpr int BAND_RW = BAND_ROWS / (BAND_NT / 64);
+template <class Hook>
+__device__ __forceinline__ void band_conv_body(const ConvArgs<bf16_t>& a, char* smem, int b, int band,
+                                               f32x16 (&acc)[BAND_RW], const Hook& ar) {
   using S = bf16_t;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NW = BAND_NT / 64, RW = BAND_ROWS / NW;
+  constexpr int RW = BAND_RW;
   S* tile = (S*)smem;
   float* tbl = (float*)(smem + band_tile_bytes());
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, px = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int b, band;
-  wg_split(blockIdx.x, 2, a.B, a.xmap, b, band);
   const int y0 = band * BAND_ROWS;
   const size_t cb = clip_off(b);
   if (tid < 32) {     // BN backward as an affine map per channel (as conv_body)
@@ -1383,13 +1388,22 @@ __global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a
       }
     }
   };
-  f32x16 acc[RW];
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i] = zero16();
+  conv_run<S, PADMAX, RW, BAND_NT>(acc, fill, a.wf, tile, nullptr, a.K, wave * RW, lane, tid, a.ablate, ar);
+}
+__global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int RW = BAND_RW;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, px = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int b, band;
+  wg_split(blockIdx.x, 2, a.B, a.xmap, b, band);
+  f32x16 acc[RW];
   bf16x4 p0[RW][4], p1[RW][4];
   const AddRowBand<RW> ar{(bf16_t*)a.out, (const bf16_t*)a.add0, (const bf16_t*)a.add1,
-                          cb + ((size_t)(y0 + wave * RW) * IMG + px) * C, h, p0, p1};
-  conv_run<S, PADMAX, RW, BAND_NT>(acc, fill, a.wf, tile, nullptr, a.K, wave * RW, lane, tid, a.ablate, ar);
+                          clip_off(b) + ((size_t)(band * BAND_ROWS + wave * RW) * IMG + px) * C, h, p0, p1};
+  band_conv_body(a, smem, b, band, acc, ar);
 }
 // -------------------------------------------------------------------------
 // Staggered two-band backward conv (r05, PT_CONV_BAND=3): the two 16-row
@@ -1446,6 +1460,63 @@ __device__ __forceinline__ void band_fill(const ConvArgs<bf16_t>& a, const float
   }
 }
 
+// Frames of several 32x32 tiles (cfg4, r06): the band tile's border pixels
+// that lie in the neighbouring tiles -- the 3 rows above band 0 / below band
+// 1 (38 px each, corners included) and 3 columns either side of the band's 19
+// image rows -- BatchNorm-backward mapped as band_fill maps the interior
+// (positions outside the frame keep the tile's zeros).  The same values
+// tile_halo gives the whole-clip conv.
+template <int NTH>
+__device__ __forceinline__ void band_halo(const ConvArgs<bf16_t>& a, const float* tbl, bf16_t* tile, int v,
+                                          int band, int tid) {
+  using S = bf16_t;
+  constexpr int CPB = 8, NCH = C / CPB, NHP = PADMAX * TILE + 19 * 2 * PADMAX;   // 114 + 114 px
+  constexpr int BATCH = 4;
+  const TileLoc L = tile_loc(v, a.ntx, a.nty);
+  const int y0 = band * BAND_ROWS;
+  for (int i0 = tid; i0 < NHP * NCH; i0 += BATCH * NTH) {
+    uint4 dv[BATCH], rv[BATCH];
+    int dst[BATCH];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int idx = i0 + k * NTH;
+      const int hp = idx / NCH, q = idx % NCH;
+      int hy, hx;
+      if (hp < PADMAX * TILE) {                         // the full rows beyond the band's image edge
+        hy = (band == 0 ? -PADMAX : IMG) + hp / TILE;
+        hx = hp % TILE - PADMAX;
+      } else {                                          // the side columns of the band's image rows
+        const int j = hp - PADMAX * TILE, sd = j % (2 * PADMAX);
+        hy = (band == 0 ? 0 : IMG - 19) + j / (2 * PADMAX);
+        hx = sd < PADMAX ? sd - PADMAX : IMG + sd - PADMAX;
+      }
+      const int dy = hy < 0 ? -1 : (hy >= IMG ? 1 : 0), dx = hx < 0 ? -1 : (hx >= IMG ? 1 : 0);
+      const bool ok = idx < NHP * NCH && L.ty + dy >= 0 && L.ty + dy < a.nty && L.tx + dx >= 0 &&
+                      L.tx + dx < a.ntx;
+      const size_t e = clip_off(ok ? v + dy * a.ntx + dx : v) +
+                       (size_t)(ok ? (hy - dy * IMG) * IMG + hx - dx * IMG : 0) * C + q * CPB;
+      dv[k] = *(const uint4*)(a.dc + e);
+      rv[k] = *(const uint4*)(a.raw + e);
+      dst[k] = ok ? tile_off<S, PADMAX>(hy - y0 + PADMAX, hx + PADMAX, q * CPB) : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      if (dst[k] < 0) continue;
+      const int ch0 = ((i0 + k * NTH) % NCH) * CPB;
+      const S* rr = (const S*)&rv[k];
+      const S* dd = (const S*)&dv[k];
+      uint4 ov;
+      S* oo = (S*)&ov;
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int ch = ch0 + j;
+        oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
+      }
+      *(uint4*)(tile + dst[k]) = ov;
+    }
+  }
+}
+
 __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t> a) {
   using S = bf16_t;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1478,17 +1549,21 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
   __syncthreads();
   PT_TR(a, a.trace_kind, 1);
   band_fill<BAND2_NT>(a, tbl, tile0, cb, 0, tid);
+  const bool tiled = a.ntx * a.nty > 1;
+  if (tiled) band_halo<BAND2_NT>(a, tbl, tile0, b, 0, tid);
   __syncthreads();
   PT_TR(a, a.trace_kind, 2);
   const int wb = wave & 3, band = wave >> 2;
   if ((PT_PRIO & 2) && band == 1) __builtin_amdgcn_s_setprio(1);   // band 1's fill + conv: the critical path
   if (band == 1) {
     band_fill<BAND2_NT / 2>(a, tbl, tile1, cb, BAND_ROWS, tid - BAND2_NT / 2);
+    if (tiled) band_halo<BAND2_NT / 2>(a, tbl, tile1, b, 1, tid - BAND2_NT / 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this wave's tile stores are done
     if (lane == 0) atomicAdd(ready, 1);
     while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
       __builtin_amdgcn_s_sleep(1);
     PT_TRT(a, a.trace_kind, 3, BAND2_NT / 2);
+    if constexpr ((PT_PRIO & 32) != 0) __builtin_amdgcn_s_setprio(0);   // band 1's conv: band 0 is critical
   }
   f32x16 acc[RW];
 #pragma unroll
@@ -2262,6 +2337,10 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     }
     PT_TRW(a, PT_K_FUSED_FB, 8);
     stag_wait<PT_FUSED_STAG_RA_FB>(cnt, wave);
+    if constexpr ((PT_PRIO & 16) != 0) {   // fb: band 0's conv is the critical path once band 1's rows are done
+      if (wave >= 4) __builtin_amdgcn_s_setprio(0);
+      else __builtin_amdgcn_s_setprio(1);
+    }
     PT_TR(a, PT_K_FUSED_FB, 3);
     fused_conv<S, true>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FB);
     PT_TR(a, PT_K_FUSED_FB, 6);
@@ -2538,6 +2617,49 @@ __global__ __launch_bounds__(PW_NT, 2) void k_pw_ba(CellArgs<S> a) {
   int b, part;
   wg_split(blockIdx.x, PWA_WGPC, a.B, a.xmap, b, part);
   pw_ba_body<S, ACT, HG, PWA_RPP>(a, smem, b, part);
+}
+
+// -------------------------------------------------------------------------
+// Fused backward A (r06; PT_CPA): k_conv_ba(t) and
+// k_pw_ba(t-1) as ONE launch of 2B workgroups.  Workgroup (clip b, part p)
+// first runs band p of the BN0-backward conv^T (k_conv_bwd_band: 16 output
+// rows, 4 waves x 4 rows; dgE_t = conv + dgEp stored as in the split form),
+// then k_pw_ba(t-1)'s rows of the same band -- k_pw_ba's workgroup (b, p)
+// owns image rows 16 p .. 16 p + 15 with wave w on rows 16 p + 4 w + i,
+// exactly the rows wave w just convolved, so every dgE row is read back by
+// the wave that stored it (program order; no barrier or flag between
+// workgroups) and the launch boundary between the two kernels goes.  The
+// two workgroups of a clip share a CU (blocks j and j + B), each at two waves
+// per SIMD.  Arithmetic, reduction slots and orders: those of
+// k_conv_bwd_band (bitwise k_conv_bwd_band2) and k_pw_ba -- bitwise the
+// split pair (tests/test_gpu_fused.py).
+// -------------------------------------------------------------------------
+static_assert(BAND_NT == PW_NT && PWA_RPP == BAND_RW && PW_NW * PWA_RPP == BAND_ROWS && PWA_WGPC == 2,
+              "a k_pw_ba workgroup's rows are one band of the banded conv");
+template <class S> constexpr int cpa_lds_bytes() {
+  return pwa_lds_bytes<S>() > band_tile_bytes() + CONV_MISC * 4 ? pwa_lds_bytes<S>()
+                                                               : band_tile_bytes() + CONV_MISC * 4;
+}
+template <int ACT, int HG>
+__global__ __launch_bounds__(PW_NT, 2) void k_conv_pw_ba(CellArgs<bf16_t> a, ConvArgs<bf16_t> c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (PT_ABL(a.ablate) & 512) return;
+  int b, part;
+  wg_split(blockIdx.x, PWA_WGPC, a.B, a.xmap, b, part);
+  {
+    constexpr int RW = BAND_RW;
+    const int lane = threadIdx.x & 63, h = lane >> 5, px = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if constexpr ((PT_PRIO & 64) != 0)        // the clip's part 1 lags: its conv beside part 0's rows
+      if (part == 1) __builtin_amdgcn_s_setprio(0); else __builtin_amdgcn_s_setprio(2);
+    f32x16 acc[RW];
+    bf16x4 p0[RW][4], p1[RW][4];
+    const AddRowBand<RW> ar{(bf16_t*)c.out, (const bf16_t*)c.add0, (const bf16_t*)c.add1,
+                            clip_off(b) + ((size_t)(part * BAND_ROWS + wave * RW) * IMG + px) * C, h, p0, p1};
+    band_conv_body(c, smem, b, part, acc, ar);
+  }
+  __syncthreads();              // the conv tile's LDS becomes k_pw_ba's
+  pw_ba_body<bf16_t, ACT, HG, PWA_RPP>(a, smem, b, part);
 }
 
 // -------------------------------------------------------------------------
@@ -4510,6 +4632,10 @@ int set_lds_attrs() {
   SETLDS((k_conv_bwd<S, PADBIG>), (conv_lds_bytes<S, PADBIG>()));
   SETLDS((k_bnbwd_fill<S>), conv_lds_bytes<S>());
   SETLDS(k_conv_bwd_band2, band2_lds_bytes());
+  SETLDS((k_conv_pw_ba<0, 0>), cpa_lds_bytes<bf16_t>());
+  SETLDS((k_conv_pw_ba<0, 1>), cpa_lds_bytes<bf16_t>());
+  SETLDS((k_conv_pw_ba<1, 0>), cpa_lds_bytes<bf16_t>());
+  SETLDS((k_conv_pw_ba<1, 1>), cpa_lds_bytes<bf16_t>());
   SETLDS((k_pw_fa<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_fb<S, 0, 0>), (pw_lds_bytes<PWF_RPP, false>()));
   SETLDS((k_pw_ba<S, 0, 0>), (pwa_lds_bytes<S>()));
@@ -4575,11 +4701,16 @@ void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
 #endif
 // 3 (r05): the staggered two-band workgroup k_conv_bwd_band2
 int band_env() { return PT_SW("PT_CONV_BAND", PT_CONV_BAND_DEF); }
+// r06: k_conv_bwd_band2 on tiled frames too (band_halo); PT_BAND2_TILED in diag builds
+#ifndef PT_BAND2_TILED_DEF
+#define PT_BAND2_TILED_DEF 0
+#endif
+bool band2_tiled_env() { return PT_SW("PT_BAND2_TILED", PT_BAND2_TILED_DEF) != 0; }
 template <class S>
 void launch_conv_bwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
   if constexpr (sizeof(S) == 2) {
     const int bm = band_env();
-    if (bm == 3 && p.K <= 2 * PADMAX + 1 && p.ntx * p.nty == 1) {
+    if (bm == 3 && p.K <= 2 * PADMAX + 1 && (p.ntx * p.nty == 1 || band2_tiled_env())) {
       hipLaunchKernelGGL(k_conv_bwd_band2, dim3(p.B), dim3(BAND2_NT), band2_lds_bytes(), st, c);
       return;
     }
@@ -4629,6 +4760,11 @@ bool pwb2_env() { return PT_SW("PT_PWB2", 1) != 0; }
 // (B=256 T=64, interleaved): 59.9-60.1 vs 58.4-58.7 us for k_pw_ba, which
 // already ran one round of workgroups (4 rows per wave); k_pw_bb2's gain came
 // from halving the rounds, not from the layout.
+// k_conv_pw_ba (r06): opt-in / default by PT_CPA_DEF; PT_CPA in diag builds
+#ifndef PT_CPA_DEF
+#define PT_CPA_DEF 0
+#endif
+bool cpa_env() { return PT_SW("PT_CPA", PT_CPA_DEF) != 0; }
 #ifndef PT_PWA2_DEF
 #define PT_PWA2_DEF 0     // A/B builds: k_pw_ba2 by default
 #endif
@@ -4872,6 +5008,9 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   const bool pwb2 = pwb2_env(), pwa2 = pwa2_env();
   const int nprod_b = p.B * (pwb2 ? (a.hgru ? pb2_wgpc<S, 1>() : pb2_wgpc<S, 0>()) : PWB_WGPC);   // BN0 bwd producers
   const int nprod_a = p.B * (pwa2 ? pa2_wgpc<S>() : PWA_WGPC);     // BN1 backward producers
+  // k_conv_pw_ba: bf16, 32x32 frames, k <= 7, the staged k_pw_ba (not k_pw_ba2)
+  const bool cpa = cpa_env() && sizeof(S) == 2 && p.K <= 2 * PADMAX + 1 && p.ntx * p.nty == 1 && !pwa2 &&
+                   PT_PWA_STAGE;
   auto launch_pwa = [&] {
     if (pwa2)
       timed(PT_K_PW_BA, st, [&] { PW_LAUNCH_NT(k_pw_ba2, dim3(nprod_a), (pa2_lds_bytes<S>()), PB2_NT); });
@@ -4913,7 +5052,24 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
       bwd_src(ca, t, 0, nprod_b);
       ca.bnw = a.bnw0; ca.fill_out = a.dci_s + t * fs;
       ca.wf = a.wt_inh; ca.out = a.dgE; ca.add0 = a.dgEp; ca.add1 = nullptr;
-      if (t >= 1) {
+      if (t >= 1 && cpa) {      // k_conv_ba(t) + k_pw_ba(t-1) in one launch
+        a.conv_done = 1;
+        a.t = t - 1;
+        if constexpr (sizeof(S) == 2)
+          timed(PT_K_CONV_PW_BA, st, [&] {
+            const dim3 g(p.B * PWA_WGPC);
+            const size_t l = cpa_lds_bytes<bf16_t>();
+            if (a.hgru) {
+              if (a.act) hipLaunchKernelGGL((k_conv_pw_ba<1, 1>), g, dim3(PW_NT), l, st, a, ca);
+              else hipLaunchKernelGGL((k_conv_pw_ba<0, 1>), g, dim3(PW_NT), l, st, a, ca);
+            } else {
+              if (a.act) hipLaunchKernelGGL((k_conv_pw_ba<1, 0>), g, dim3(PW_NT), l, st, a, ca);
+              else hipLaunchKernelGGL((k_conv_pw_ba<0, 0>), g, dim3(PW_NT), l, st, a, ca);
+            } });
+        if (stop()) return 0;
+        if (int rc = sync_bwd(t - 1, 1, nprod_a)) return rc;
+        continue;
+      } else if (t >= 1) {
         timed(PT_K_CONV_BA, st, [&] {
           launch_conv_bwd<S>(p, st, ca); });
         a.conv_done = 1;
@@ -5039,7 +5195,8 @@ int pt_cell_backward_dist(const pt_cell_desc* d, const void* x, const pt_cell_pa
       if ((rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>())) return rc;
       ptg::Key k;
       k.add(phase).add(wsplit).add(*d).add(x).add(*p).add(saved).add(ws).add(d_e_last).add(*g).add(ablate_env())
-          .add(band_env()).add(pwb2_env()).add(pwa2_env()).add(xmap_env()).add(wg16_env()).add(wgdma_env());
+          .add(band_env()).add(pwb2_env()).add(pwa2_env()).add(xmap_env()).add(wg16_env()).add(wgdma_env())
+          .add(cpa_env()).add(band2_tiled_env());
       rc = g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
     }
     if (rc) return rc;

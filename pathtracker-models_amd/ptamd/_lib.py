@@ -34,7 +34,7 @@ EXPORTS = ("pt_cell_saved_bytes", "pt_cell_workspace_bytes", "pt_cell_forward",
 # kernel kinds for pt_cell_timing_* (include/pt_cell.h)
 KIND_NAMES = ("k_pw_fa", "k_conv_fa", "k_pw_fb", "k_conv_fb", "k_pw_ba", "k_conv_ba",
               "k_pw_bb", "k_conv_bb", "k_wgrad", "k_prep", "k_reduce", "k_fused_fa",
-              "k_fused_fb", "k_persist_fwd")
+              "k_fused_fb", "k_persist_fwd", "k_conv_pw_ba")
 NKINDS = len(KIND_NAMES)
 TRACE_WG, TRACE_SLOTS = 2048, 32      # pt_cell_trace record layout (csrc/pt_cell.hip PT_TR)
 

@@ -26,8 +26,9 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _run(m, x, y, fused, persist=False, band=False):
-    with variants(PT_CELL_FUSED=int(fused), PT_CELL_PERSIST=int(persist), PT_CONV_BAND=int(band)):
+def _run(m, x, y, fused, persist=False, band=False, cpa=0, band2_tiled=0):
+    with variants(PT_CELL_FUSED=int(fused), PT_CELL_PERSIST=int(persist), PT_CONV_BAND=int(band),
+                  PT_CPA=int(cpa), PT_BAND2_TILED=int(band2_tiled)):
         m.zero_grad(set_to_none=True)
         out, _ = m(x)
         F.binary_cross_entropy_with_logits(out, y.reshape(-1, 1)).backward()
@@ -65,6 +66,44 @@ def test_staggered_two_band_conv_is_bitwise_the_whole_clip_conv(cell, act, b, t)
     8-wave workgroup, band 1 filled under band 0's MFMAs, an LDS counter
     instead of a workgroup barrier for band 1's waves) against k_conv_bwd."""
     _compare(cell, act, b, t, dict(fused=True, band=3))
+
+
+@pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("int", "tanh", 5, 3),
+                                          ("hgru", "softplus", 16, 6), ("int", "softplus", 256, 64)])
+def test_fused_backward_a_is_bitwise_the_split_pair(cell, act, b, t):
+    """k_conv_pw_ba (PT_CPA=1, r06: k_conv_ba(t)'s band p and k_pw_ba(t-1)'s
+    rows of that band in one workgroup, one launch per frame) against the
+    split k_conv_bwd_band2 + k_pw_ba: the same arithmetic and reduction slots."""
+    _compare(cell, act, b, t, dict(fused=True, cpa=1))
+
+
+@pytest.mark.parametrize("hw,b,t", [(64, 4, 6), (96, 2, 4)])
+def test_staggered_two_band_conv_on_tiled_frames_is_bitwise_the_whole_clip_conv(hw, b, t):
+    """k_conv_bwd_band2 on frames of several 32x32 tiles (PT_BAND2_TILED=1,
+    r06: the band tile's border from the neighbouring tiles, band_halo)
+    against the whole-clip conv with tile_halo (hGRU, cfg4's 64x64 and a
+    3x3-tile 96x96 frame whose middle tile has neighbours on every side)."""
+    from models import ffhgru_hierarchy as hg
+    dev = _dev()
+    torch.manual_seed(hw + b)
+    m = hg.FFhGRU(dimensions=32, timesteps=t, kernel_size=7)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
+                p.uniform_(0.5, 1.5)
+            elif n.endswith(("mu", "gamma")):
+                p.uniform_(-0.5, 0.5)
+    m = m.to(dev)
+    m.cell_dtype = "bf16"
+    x = torch.rand(b, 3, t, hw, hw, device=dev)
+    y = (torch.arange(b, device=dev) % 2).float()
+    o1, s1, g1, gr1 = _run(m, x, y, fused=True, band=0)
+    o0, s0, g0, gr0 = _run(m, x, y, fused=True, band=3, band2_tiled=1)
+    assert torch.isfinite(o1).all()
+    assert torch.equal(o1, o0), (o1 - o0).abs().max().item()
+    bad = {k: ((gr1[k] - gr0[k]).abs().max() / gr0[k].abs().max().clamp_min(1e-30)).item()
+           for k in gr0 if k.startswith(("unit1.", "preproc.")) and not torch.equal(gr1[k], gr0[k])}
+    assert not bad, bad
 
 
 def _compare(cell, act, b, t, other):
