@@ -70,7 +70,7 @@ def gate_flops():          # one 1x1 C->C gate conv over one clip frame
     return 2 * C * C * HW * HW
 
 
-def algorithmic_flops(kind, batch, frames, fused=False):
+def algorithmic_flops(kind, batch, frames, fused=False, cpa=False):
     """Algorithmic FLOPs of ALL launches of one kernel kind in one step.
 
     Counts the model's contractions only (no recompute): forward conv + gates;
@@ -78,8 +78,13 @@ def algorithmic_flops(kind, batch, frames, fused=False):
     in k_wgrad.  Sum over kinds = 3 x forward (41.9 GFLOP/clip
     at T=64, minus the stem's 12.6 MFLOP which is counted nowhere).  fused: the
     forward runs as k_fused_fa / k_fused_fb (point-wise + conv per launch) and
-    one k_pw_fa that only closes the last frame."""
+    one k_pw_fa that only closes the last frame.  cpa (r06): k_conv_ba(t) and
+    k_pw_ba(t-1) run as one k_conv_pw_ba launch for t = T-1 .. 1; k_pw_ba
+    keeps the first (head only) and last (frame 0's tail: no attention gates
+    for InT, gE_0 = 0) launches."""
     cf, gf = conv_flops(), gate_flops()
+    if cpa and kind in ("k_conv_pw_ba", "k_conv_ba", "k_pw_ba"):
+        return {"k_conv_pw_ba": (frames - 1) * (cf + 4 * gf)}.get(kind, 0) * batch
     if fused:
         fwd = {"k_fused_fa": frames * (cf + 4 * gf), "k_fused_fb": frames * (cf + 2 * gf)}
         if kind in fwd or kind in ("k_pw_fa", "k_pw_fb", "k_conv_fa", "k_conv_fb"):
@@ -98,7 +103,7 @@ def algorithmic_flops(kind, batch, frames, fused=False):
     return per_clip.get(kind, 0) * batch
 
 
-def algorithmic_bytes(kind, batch, frames, elt, xb=4, fused=False):
+def algorithmic_bytes(kind, batch, frames, elt, xb=4, fused=False, cpa=False):
     """Algorithmic HBM bytes of ALL launches of one kernel kind in one step
     (DESIGN.md §3 table): F = one clip-frame state tensor (32x32x32 elements),
     XF = one clip-frame of the input (3x32x32; xb = 4 B f32, 1 B raw u8 clips).
@@ -119,6 +124,12 @@ def algorithmic_bytes(kind, batch, frames, elt, xb=4, fused=False):
                "k_pw_fa": 5 * F + 2 * dE}                # closes E_{T-1} only
         if kind in fwd or kind in ("k_pw_fb", "k_conv_fa", "k_conv_fb"):
             return fwd.get(kind, 0) * batch
+    if cpa and kind in ("k_conv_pw_ba", "k_conv_ba", "k_pw_ba"):
+        # k_conv_pw_ba: the two kernels' bytes (dgE still stored and read back,
+        # by the same wave); k_pw_ba: its first and last launches ~ one frame;
+        # k_conv_ba: frame 0's BatchNorm-backward fill (dc, raw in, dci out)
+        return {"k_conv_pw_ba": (frames - 1) * (5 * F + XF + 11 * F + dE),
+                "k_pw_ba": XF + 11 * F + dE, "k_conv_ba": 3 * F}[kind] * batch
     per_clip = {
         "k_pw_fa": frames * (XF + 7 * F + 2 * dE),
         "k_conv_fa": frames * 2 * F,
@@ -141,7 +152,7 @@ FLOP_8D_FRAME = 2 * conv_flops() + 6 * gate_flops()
 FLOP_8D_STEM = 2 * 3 * C * HW * HW
 BYTES_8D_FRAME = 17.2e6 / 64
 CONV_KINDS = ("k_fused_fa", "k_fused_fb", "k_conv_fa", "k_conv_fb", "k_conv_ba", "k_conv_bb", "k_wgrad",
-              "k_persist_fwd")
+              "k_persist_fwd", "k_conv_pw_ba")
 
 
 def step_flops_8d(batch, frames):
@@ -274,7 +285,7 @@ def cpu_baseline(seconds, frames=64, batch=4):
                       f"{n} steps in {el:.1f}s"}
 
 
-def kernel_roofline(kind, ms, n, batch, frames, steps, dtype, xb, fused=False):
+def kernel_roofline(kind, ms, n, batch, frames, steps, dtype, xb, fused=False, cpa=False):
     """One kernel kind against the roofline SURVEY.md §8(d) binds it to: every
     kernel that runs a k x k conv (the fused cell segments, the backward convs,
     the weight gradients) is MFMA-bound -- achieved = §8(d) FLOPs per launch /
@@ -283,8 +294,8 @@ def kernel_roofline(kind, ms, n, batch, frames, steps, dtype, xb, fused=False):
     returned for every kernel: its MFMA fraction and, labelled as the
     design's own byte count, its HBM fraction."""
     elt = 2 if dtype == "bf16" else 4
-    fl = algorithmic_flops(kind, batch, frames, fused) * steps / max(n, 1)
-    by = algorithmic_bytes(kind, batch, frames, elt, xb, fused) * steps / max(n, 1)
+    fl = algorithmic_flops(kind, batch, frames, fused, cpa) * steps / max(n, 1)
+    by = algorithmic_bytes(kind, batch, frames, elt, xb, fused, cpa) * steps / max(n, 1)
     avg = ms / max(n, 1) * 1e-3
     peak_f = PEAK_TFLOPS[dtype]
     mf = fl / avg / 1e12
@@ -433,10 +444,11 @@ def main():
         xb = 1 if args.input == "u8" else 4
         value = world * args.batch * args.steps / el
         fused = kern["k_fused_fa"][1] > 0
+        cpa = kern.get("k_conv_pw_ba", (0.0, 0))[1] > 0
         dom = max(kern, key=lambda k: kern[k][0])
         dom_ms, dom_n = kern[dom]
         roof, fl, by, avg_ms = kernel_roofline(dom, dom_ms, dom_n, args.batch, args.frames,
-                                               args.steps, args.dtype, xb, fused)
+                                               args.steps, args.dtype, xb, fused, cpa)
         roof.update({"traffic": pmc_traffic(dom, args.batch, args.frames, args.dtype, version),
                      "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
                      "algorithmic_flop_per_launch": fl, "algorithmic_bytes_per_launch": by})
@@ -444,11 +456,11 @@ def main():
         # dominant one above): conv / wgrad are MFMA-bound, point-wise HBM-bound
         per_kind = {}
         for k, (ms, n) in kern.items():
-            if n == 0 or ms <= 0 or (algorithmic_flops(k, 1, args.frames, fused) == 0 and
-                                     algorithmic_bytes(k, 1, args.frames, 2, 4, fused) == 0):
+            if n == 0 or ms <= 0 or (algorithmic_flops(k, 1, args.frames, fused, cpa) == 0 and
+                                     algorithmic_bytes(k, 1, args.frames, 2, 4, fused, cpa) == 0):
                 continue
             r, _, _, a = kernel_roofline(k, ms, n, args.batch, args.frames, args.steps,
-                                         args.dtype, xb, fused)
+                                         args.dtype, xb, fused, cpa)
             per_kind[k] = {"bound": r["bound"], "achieved": r["achieved"], "unit": r["unit"],
                            "frac": r["frac"], "mfma_frac": r["mfma_frac"],
                            "hbm_frac_design_bytes": r["hbm_frac_design_bytes"],

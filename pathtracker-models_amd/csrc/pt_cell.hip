@@ -4701,9 +4701,11 @@ void launch_conv_fwd(const Plan& p, hipStream_t st, const ConvArgs<S>& c) {
 #endif
 // 3 (r05): the staggered two-band workgroup k_conv_bwd_band2
 int band_env() { return PT_SW("PT_CONV_BAND", PT_CONV_BAND_DEF); }
-// r06: k_conv_bwd_band2 on tiled frames too (band_halo); PT_BAND2_TILED in diag builds
+// r06: k_conv_bwd_band2 on tiled frames too (band_halo; default); PT_BAND2_TILED=0
+// in diag builds selects the whole-clip conv.  cfg4 (profiles/r06_bench_cpa.txt):
+// conv_ba + conv_bb 17.94 -> 17.00 ms per step, 1,450 -> 1,469 clips/s
 #ifndef PT_BAND2_TILED_DEF
-#define PT_BAND2_TILED_DEF 0
+#define PT_BAND2_TILED_DEF 1
 #endif
 bool band2_tiled_env() { return PT_SW("PT_BAND2_TILED", PT_BAND2_TILED_DEF) != 0; }
 template <class S>
@@ -4760,9 +4762,12 @@ bool pwb2_env() { return PT_SW("PT_PWB2", 1) != 0; }
 // (B=256 T=64, interleaved): 59.9-60.1 vs 58.4-58.7 us for k_pw_ba, which
 // already ran one round of workgroups (4 rows per wave); k_pw_bb2's gain came
 // from halving the rounds, not from the layout.
-// k_conv_pw_ba (r06): opt-in / default by PT_CPA_DEF; PT_CPA in diag builds
+// k_conv_pw_ba (r06, default): PT_CPA=0 in diag builds selects the split
+// k_conv_bwd_band2 + k_pw_ba.  A/B (profiles/r06_libab_cpa.txt,
+// r06_bench_cpa.txt): 81.4 us per launch vs 31.7 + 53.9 us split, bench
+// 20.06 vs 20.11-20.17 ms per step on one box, alternating
 #ifndef PT_CPA_DEF
-#define PT_CPA_DEF 0
+#define PT_CPA_DEF 1
 #endif
 bool cpa_env() { return PT_SW("PT_CPA", PT_CPA_DEF) != 0; }
 #ifndef PT_PWA2_DEF

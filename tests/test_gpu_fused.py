@@ -11,7 +11,11 @@ fused segments in one launch, the BatchNorm syncs as in-launch waits on the
 deterministic group sums) is the same arithmetic in the same reduction order,
 so it too must reproduce the per-segment launches bit for bit.  So must the
 banded backward convs (PT_CONV_BAND=1, and the staggered two-band workgroup,
-PT_CONV_BAND=3): per output row the same MFMA order."""
+PT_CONV_BAND=3): per output row the same MFMA order.  r06: the fused
+backward A (k_conv_pw_ba, the default; PT_CPA=0 selects the split pair) and
+the two-band conv on tiled frames (PT_BAND2_TILED) likewise.  The baseline
+of every comparison is the library's defaults with the whole-clip backward
+conv (PT_CONV_BAND=0)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -26,7 +30,7 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _run(m, x, y, fused, persist=False, band=False, cpa=0, band2_tiled=0):
+def _run(m, x, y, fused, persist=False, band=False, cpa=1, band2_tiled=1):
     with variants(PT_CELL_FUSED=int(fused), PT_CELL_PERSIST=int(persist), PT_CONV_BAND=int(band),
                   PT_CPA=int(cpa), PT_BAND2_TILED=int(band2_tiled)):
         m.zero_grad(set_to_none=True)
@@ -71,10 +75,11 @@ def test_staggered_two_band_conv_is_bitwise_the_whole_clip_conv(cell, act, b, t)
 @pytest.mark.parametrize("cell,act,b,t", [("int", "softplus", 24, 8), ("int", "tanh", 5, 3),
                                           ("hgru", "softplus", 16, 6), ("int", "softplus", 256, 64)])
 def test_fused_backward_a_is_bitwise_the_split_pair(cell, act, b, t):
-    """k_conv_pw_ba (PT_CPA=1, r06: k_conv_ba(t)'s band p and k_pw_ba(t-1)'s
+    """k_conv_pw_ba (the r06 default: k_conv_ba(t)'s band p and k_pw_ba(t-1)'s
     rows of that band in one workgroup, one launch per frame) against the
-    split k_conv_bwd_band2 + k_pw_ba: the same arithmetic and reduction slots."""
-    _compare(cell, act, b, t, dict(fused=True, cpa=1))
+    split k_conv_bwd_band2 + k_pw_ba (PT_CPA=0): the same arithmetic and
+    reduction slots."""
+    _compare(cell, act, b, t, dict(fused=True, cpa=0))
 
 
 @pytest.mark.parametrize("hw,b,t", [(64, 4, 6), (96, 2, 4)])
@@ -97,7 +102,7 @@ def test_staggered_two_band_conv_on_tiled_frames_is_bitwise_the_whole_clip_conv(
     m.cell_dtype = "bf16"
     x = torch.rand(b, 3, t, hw, hw, device=dev)
     y = (torch.arange(b, device=dev) % 2).float()
-    o1, s1, g1, gr1 = _run(m, x, y, fused=True, band=0)
+    o1, s1, g1, gr1 = _run(m, x, y, fused=True, band=0, band2_tiled=0)
     o0, s0, g0, gr0 = _run(m, x, y, fused=True, band=3, band2_tiled=1)
     assert torch.isfinite(o1).all()
     assert torch.equal(o1, o0), (o1 - o0).abs().max().item()
@@ -127,7 +132,7 @@ def _compare(cell, act, b, t, other):
     clips, labels = synth.make_batch(b * 7 + t, b, t)
     x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float().to(dev)
     y = torch.tensor([ord(v) for v in labels], dtype=torch.float32, device=dev)
-    o1, s1, g1, gr1 = _run(m, x, y, fused=True)
+    o1, s1, g1, gr1 = _run(m, x, y, fused=True)        # the library defaults
     o0, s0, g0, gr0 = _run(m, x, y, **other)
     assert torch.isfinite(o1).all()
     for name, u, v in (("logits", o1, o0), ("states", s1, s0), ("gates", g1, g0)):
