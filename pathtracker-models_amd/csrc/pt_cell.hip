@@ -1317,6 +1317,63 @@ struct AddRowBand {
   }
 };
 
+// Frames of several 32x32 tiles (cfg4, r06): the band tile's border pixels
+// that lie in the neighbouring tiles -- the 3 rows above band 0 / below band
+// 1 (38 px each, corners included) and 3 columns either side of the band's 19
+// image rows -- BatchNorm-backward mapped as band_fill maps the interior
+// (positions outside the frame keep the tile's zeros).  The same values
+// tile_halo gives the whole-clip conv.
+template <int NTH>
+__device__ __forceinline__ void band_halo(const ConvArgs<bf16_t>& a, const float* tbl, bf16_t* tile, int v,
+                                          int band, int tid) {
+  using S = bf16_t;
+  constexpr int CPB = 8, NCH = C / CPB, NHP = PADMAX * TILE + 19 * 2 * PADMAX;   // 114 + 114 px
+  constexpr int BATCH = 4;
+  const TileLoc L = tile_loc(v, a.ntx, a.nty);
+  const int y0 = band * BAND_ROWS;
+  for (int i0 = tid; i0 < NHP * NCH; i0 += BATCH * NTH) {
+    uint4 dv[BATCH], rv[BATCH];
+    int dst[BATCH];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int idx = i0 + k * NTH;
+      const int hp = idx / NCH, q = idx % NCH;
+      int hy, hx;
+      if (hp < PADMAX * TILE) {                         // the full rows beyond the band's image edge
+        hy = (band == 0 ? -PADMAX : IMG) + hp / TILE;
+        hx = hp % TILE - PADMAX;
+      } else {                                          // the side columns of the band's image rows
+        const int j = hp - PADMAX * TILE, sd = j % (2 * PADMAX);
+        hy = (band == 0 ? 0 : IMG - 19) + j / (2 * PADMAX);
+        hx = sd < PADMAX ? sd - PADMAX : IMG + sd - PADMAX;
+      }
+      const int dy = hy < 0 ? -1 : (hy >= IMG ? 1 : 0), dx = hx < 0 ? -1 : (hx >= IMG ? 1 : 0);
+      const bool ok = idx < NHP * NCH && L.ty + dy >= 0 && L.ty + dy < a.nty && L.tx + dx >= 0 &&
+                      L.tx + dx < a.ntx;
+      const size_t e = clip_off(ok ? v + dy * a.ntx + dx : v) +
+                       (size_t)(ok ? (hy - dy * IMG) * IMG + hx - dx * IMG : 0) * C + q * CPB;
+      dv[k] = *(const uint4*)(a.dc + e);
+      rv[k] = *(const uint4*)(a.raw + e);
+      dst[k] = ok ? tile_off<S, PADMAX>(hy - y0 + PADMAX, hx + PADMAX, q * CPB) : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      if (dst[k] < 0) continue;
+      const int ch0 = ((i0 + k * NTH) % NCH) * CPB;
+      const S* rr = (const S*)&rv[k];
+      const S* dd = (const S*)&dv[k];
+      uint4 ov;
+      S* oo = (S*)&ov;
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int ch = ch0 + j;
+        oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
+      }
+      *(uint4*)(tile + dst[k]) = ov;
+    }
+  }
+}
+
 // The band's conv with a row hook (hook(i, acc): output row i finished;
 // k_conv_bwd_band adds the addends and stores, k_conv_pw_ba keeps the row).
 constexpr int BAND_RW = BAND_ROWS / (BAND_NT / 64);
@@ -1387,6 +1444,7 @@ __device__ __forceinline__ void band_conv_body(const ConvArgs<bf16_t>& a, char* 
         *(uint4*)(tile + tile_off<S, PADMAX>(y - y0 + PADMAX, x + PADMAX, ch0)) = ov;
       }
     }
+    if (a.ntx * a.nty > 1) band_halo<BAND_NT>(a, tbl, tile, b, band, tid);   // tiled frames (r06)
   };
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i] = zero16();
@@ -1456,63 +1514,6 @@ __device__ __forceinline__ void band_fill(const ConvArgs<bf16_t>& a, const float
       if (y >= y0 && y < y0 + BAND_ROWS)          // each pixel written out by one band
         *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
       *(uint4*)(tile + tile_off<S, PADMAX>(y - y0 + PADMAX, x + PADMAX, ch0)) = ov;
-    }
-  }
-}
-
-// Frames of several 32x32 tiles (cfg4, r06): the band tile's border pixels
-// that lie in the neighbouring tiles -- the 3 rows above band 0 / below band
-// 1 (38 px each, corners included) and 3 columns either side of the band's 19
-// image rows -- BatchNorm-backward mapped as band_fill maps the interior
-// (positions outside the frame keep the tile's zeros).  The same values
-// tile_halo gives the whole-clip conv.
-template <int NTH>
-__device__ __forceinline__ void band_halo(const ConvArgs<bf16_t>& a, const float* tbl, bf16_t* tile, int v,
-                                          int band, int tid) {
-  using S = bf16_t;
-  constexpr int CPB = 8, NCH = C / CPB, NHP = PADMAX * TILE + 19 * 2 * PADMAX;   // 114 + 114 px
-  constexpr int BATCH = 4;
-  const TileLoc L = tile_loc(v, a.ntx, a.nty);
-  const int y0 = band * BAND_ROWS;
-  for (int i0 = tid; i0 < NHP * NCH; i0 += BATCH * NTH) {
-    uint4 dv[BATCH], rv[BATCH];
-    int dst[BATCH];
-#pragma unroll
-    for (int k = 0; k < BATCH; ++k) {
-      const int idx = i0 + k * NTH;
-      const int hp = idx / NCH, q = idx % NCH;
-      int hy, hx;
-      if (hp < PADMAX * TILE) {                         // the full rows beyond the band's image edge
-        hy = (band == 0 ? -PADMAX : IMG) + hp / TILE;
-        hx = hp % TILE - PADMAX;
-      } else {                                          // the side columns of the band's image rows
-        const int j = hp - PADMAX * TILE, sd = j % (2 * PADMAX);
-        hy = (band == 0 ? 0 : IMG - 19) + j / (2 * PADMAX);
-        hx = sd < PADMAX ? sd - PADMAX : IMG + sd - PADMAX;
-      }
-      const int dy = hy < 0 ? -1 : (hy >= IMG ? 1 : 0), dx = hx < 0 ? -1 : (hx >= IMG ? 1 : 0);
-      const bool ok = idx < NHP * NCH && L.ty + dy >= 0 && L.ty + dy < a.nty && L.tx + dx >= 0 &&
-                      L.tx + dx < a.ntx;
-      const size_t e = clip_off(ok ? v + dy * a.ntx + dx : v) +
-                       (size_t)(ok ? (hy - dy * IMG) * IMG + hx - dx * IMG : 0) * C + q * CPB;
-      dv[k] = *(const uint4*)(a.dc + e);
-      rv[k] = *(const uint4*)(a.raw + e);
-      dst[k] = ok ? tile_off<S, PADMAX>(hy - y0 + PADMAX, hx + PADMAX, q * CPB) : -1;
-    }
-#pragma unroll
-    for (int k = 0; k < BATCH; ++k) {
-      if (dst[k] < 0) continue;
-      const int ch0 = ((i0 + k * NTH) % NCH) * CPB;
-      const S* rr = (const S*)&rv[k];
-      const S* dd = (const S*)&dv[k];
-      uint4 ov;
-      S* oo = (S*)&ov;
-#pragma unroll
-      for (int j = 0; j < CPB; ++j) {
-        const int ch = ch0 + j;
-        oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
-      }
-      *(uint4*)(tile + dst[k]) = ov;
     }
   }
 }
@@ -5014,8 +5015,8 @@ int run_backward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr,
   const int nprod_b = p.B * (pwb2 ? (a.hgru ? pb2_wgpc<S, 1>() : pb2_wgpc<S, 0>()) : PWB_WGPC);   // BN0 bwd producers
   const int nprod_a = p.B * (pwa2 ? pa2_wgpc<S>() : PWA_WGPC);     // BN1 backward producers
   // k_conv_pw_ba: bf16, 32x32 frames, k <= 7, the staged k_pw_ba (not k_pw_ba2)
-  const bool cpa = cpa_env() && sizeof(S) == 2 && p.K <= 2 * PADMAX + 1 && p.ntx * p.nty == 1 && !pwa2 &&
-                   PT_PWA_STAGE;
+  const bool cpa = cpa_env() && sizeof(S) == 2 && p.K <= 2 * PADMAX + 1 &&
+                   (p.ntx * p.nty == 1 || band2_tiled_env()) && !pwa2 && PT_PWA_STAGE;
   auto launch_pwa = [&] {
     if (pwa2)
       timed(PT_K_PW_BA, st, [&] { PW_LAUNCH_NT(k_pw_ba2, dim3(nprod_a), (pa2_lds_bytes<S>()), PB2_NT); });

@@ -82,12 +82,13 @@ def test_fused_backward_a_is_bitwise_the_split_pair(cell, act, b, t):
     _compare(cell, act, b, t, dict(fused=True, cpa=0))
 
 
-@pytest.mark.parametrize("hw,b,t", [(64, 4, 6), (96, 2, 4)])
-def test_staggered_two_band_conv_on_tiled_frames_is_bitwise_the_whole_clip_conv(hw, b, t):
+@pytest.mark.parametrize("hw,b,t,cpa", [(64, 4, 6, 0), (64, 4, 6, 1), (96, 2, 4, 1)])
+def test_staggered_two_band_conv_on_tiled_frames_is_bitwise_the_whole_clip_conv(hw, b, t, cpa):
     """k_conv_bwd_band2 on frames of several 32x32 tiles (PT_BAND2_TILED=1,
-    r06: the band tile's border from the neighbouring tiles, band_halo)
-    against the whole-clip conv with tile_halo (hGRU, cfg4's 64x64 and a
-    3x3-tile 96x96 frame whose middle tile has neighbours on every side)."""
+    r06: the band tile's border from the neighbouring tiles, band_halo), and
+    with cpa the fused backward A on them too, against the whole-clip convs
+    with tile_halo and the split k_pw_ba (hGRU, cfg4's 64x64 and a 3x3-tile
+    96x96 frame whose middle tile has neighbours on every side)."""
     from models import ffhgru_hierarchy as hg
     dev = _dev()
     torch.manual_seed(hw + b)
@@ -102,8 +103,8 @@ def test_staggered_two_band_conv_on_tiled_frames_is_bitwise_the_whole_clip_conv(
     m.cell_dtype = "bf16"
     x = torch.rand(b, 3, t, hw, hw, device=dev)
     y = (torch.arange(b, device=dev) % 2).float()
-    o1, s1, g1, gr1 = _run(m, x, y, fused=True, band=0, band2_tiled=0)
-    o0, s0, g0, gr0 = _run(m, x, y, fused=True, band=3, band2_tiled=1)
+    o1, s1, g1, gr1 = _run(m, x, y, fused=True, band=0, band2_tiled=0, cpa=0)
+    o0, s0, g0, gr0 = _run(m, x, y, fused=True, band=3, band2_tiled=1, cpa=cpa)
     assert torch.isfinite(o1).all()
     assert torch.equal(o1, o0), (o1 - o0).abs().max().item()
     bad = {k: ((gr1[k] - gr0[k]).abs().max() / gr0[k].abs().max().clamp_min(1e-30)).item()
