@@ -480,6 +480,12 @@ struct CellArgs {
   float* slab;                          // [B][PW_PARTS][SLAB]
   int conv_done;                        // k_pw_ba: dgE holds conv^T(w_inh) + dgEp
   int xmap;                             // XCD-affine workgroup order (wg_split)
+  // fused forward on tiled frames (xb_exchange): each tile's 348 border pixels
+  // of its conv input [B][348][32], the per-segment flags [2][B] (t + 1 once
+  // published; zeroed per call) and the give-up word
+  S* xch;
+  unsigned* xflag;
+  unsigned* xerr;
 };
 
 // Workgroup j of a launch with nper workgroups per clip -> (clip b, part).
@@ -815,6 +821,82 @@ __device__ __forceinline__ void tile_halo(S* __restrict__ tile, int v, int ntx, 
     for (int kk = 0; kk < BATCH; ++kk)
       if (dst[kk] >= 0) *(u32x4*)(tile + dst[kk]) = val[kk];
   }
+}
+
+// Fused forward on tiled frames (r06, VERDICT r05 next #5a).  The conv's 3-px
+// halo is the point-wise output of the neighbouring tiles' workgroups in the
+// SAME launch.  After its rows every tile workgroup copies the 348 border
+// pixels of its conv input (rows 0-2 and 29-31, columns 0-2 and 29-31 of its
+// LDS tile) to its slot of xch with write-through (agent-scope) stores and,
+// once they are acknowledged, sets its flag to t + 1; it then waits for the
+// flags of its (up to 8) neighbours and fills its halo from their slots with
+// agent-coherent loads (a neighbour may run on another XCD: no L2 is shared,
+// the same protocol as the BatchNorm partials).  No grid barrier and no
+// co-residency requirement: each XCD dispatches its workgroups in index
+// order, so every workgroup resident on the XCD of the lowest not-yet-resident
+// tile belongs to a lower clip, all of whose tiles are resident or done --
+// they finish and free the slot.  The waits are bounded all the same: a
+// give-up sets *xerr and fills the halo with NaN, so a broken assumption shows
+// up as NaN results, never as a hang.  Same bf16 values as tile_halo reads
+// from the stored conv input: bitwise the split tiled forward.
+constexpr int XB_PIX = 6 * IMG + 6 * (IMG - 6);   // 348 border pixels of a 32x32 tile
+__device__ __forceinline__ int xb_index(int ly, int lx) {
+  if (ly < 3) return ly * IMG + lx;
+  if (ly >= IMG - 3) return 3 * IMG + (ly - (IMG - 3)) * IMG + lx;
+  return 6 * IMG + (ly - 3) * 6 + (lx < 3 ? lx : lx - (IMG - 6));
+}
+__device__ __forceinline__ void xb_pixel(int i, int& ly, int& lx) {
+  if (i < 3 * IMG) { ly = i / IMG; lx = i % IMG; return; }
+  if (i < 6 * IMG) { const int j = i - 3 * IMG; ly = IMG - 3 + j / IMG; lx = j % IMG; return; }
+  const int j = i - 6 * IMG, q = j % 6;
+  ly = 3 + j / 6;
+  lx = q < 3 ? q : IMG - 6 + q;
+}
+template <class S, int NTH>
+__device__ void xb_exchange(const CellArgs<S>& a, S* tile, unsigned* flags, int v, int t, int tid) {
+  static_assert(sizeof(S) == 2, "the fused forward is bf16");
+  // publish: 348 px x 8 quads of 4 channels (8 B), write-through
+  uint64_t* dst = (uint64_t*)(a.xch + (size_t)v * XB_PIX * C);
+  for (int w = tid; w < XB_PIX * 8; w += NTH) {
+    int ly, lx;
+    xb_pixel(w >> 3, ly, lx);
+    const uint64_t val = *(const uint64_t*)(tile + tile_off<S, PADMAX>(ly + PADMAX, lx + PADMAX, 4 * (w & 7)));
+    __hip_atomic_store(dst + w, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // acknowledged
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(flags + v, (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // wait: lane 3 (dy + 1) + (dx + 1) of wave 0 polls neighbour (dy, dx)
+  const TileLoc L = tile_loc(v, a.ntx, a.nty);
+  int bad = 0;
+  if (tid < 9 && tid != 4) {
+    const int dy = tid / 3 - 1, dx = tid % 3 - 1;
+    if (L.ty + dy >= 0 && L.ty + dy < a.nty && L.tx + dx >= 0 && L.tx + dx < a.ntx) {
+      const unsigned* f = flags + v + dy * a.ntx + dx;
+      for (unsigned it = 1; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1);
+           ++it) {
+        if ((it & 255) == 0 &&         // ~0.3 s, or another workgroup already gave up
+            (it > (1u << 18) || __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          bad = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  const bool poison = __syncthreads_or(bad);
+  if (poison && tid == 0) __hip_atomic_store(a.xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the halo from the neighbours' slots (agent-coherent 8-B loads)
+  const uint64_t* src = (const uint64_t*)a.xch;
+  tile_halo<S, PADMAX, NTH>(tile, v, a.ntx, a.nty, 0, tid, [&](size_t e, int) {
+    const size_t nb = e / ((size_t)NPIX * C);
+    const int r = (int)(e - nb * NPIX * C), pix = r / C, ch = r % C;
+    const uint64_t* p = src + ((nb * XB_PIX + xb_index(pix / IMG, pix % IMG)) * C + ch) / 4;
+    if (poison) return u32x4{0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
+    const uint64_t lo = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  });
 }
 
 // Stem (models/InT.py:212-213): z = W_pre x + b; xbn = nl(z); CL layout.
@@ -2146,21 +2228,26 @@ __device__ __forceinline__ FusedLds fused_carve(char* smem) {
 
 // The conv half: conv(tile, wf) for this wave's rows, rows stored as they
 // finish (out_raw), then the per-clip BN partials (bnout).
-template <class S, bool NOBAR = false>
+template <class S, bool NOBAR = false, bool XB = false>
 __device__ __forceinline__ void fused_conv(const CellArgs<S>& a, const ConvArgs<S>& c, S* out_raw,
                                            const BnSlot& bnout, char* smem, const FusedLds& L, int b,
-                                           int wave, int lane, int tid, int kind) {
+                                           int wave, int lane, int tid, int kind, unsigned* xflags = nullptr) {
   constexpr int RW = FUSED_RW;
   f32x16 acc[RW];
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i] = zero16();
   const int h = lane >> 5, px = lane & 31;
   const StoreRow<S> sr{out_raw + clip_off(b) + ((size_t)(wave * RW) * IMG + px) * C, h, false};
-  auto nofill = [](int) {};                 // the point-wise half filled the tile
+  // the point-wise half filled the tile's interior; tiled frames: the halo
+  // from the neighbouring tiles' workgroups (xb_exchange), between the
+  // conv's two barriers
+  auto fill = [&](int) {
+    if constexpr (XB && sizeof(S) == 2) xb_exchange<S, CONV_NT>(a, (S*)L.tile, xflags, b, a.t, tid);
+  };
   if constexpr (NOBAR)                      // (the caller waited for this wave's input rows)
     conv_run_nobar<S, RW, CONV_NT>(acc, c.wf, (S*)L.tile, a.K, wave * RW, lane, tid, PT_ABL(a.ablate) & 1, sr);
   else
-    conv_run<S, PADMAX, RW, CONV_NT>(acc, nofill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
+    conv_run<S, PADMAX, RW, CONV_NT>(acc, fill, c.wf, (S*)L.tile, nullptr, a.K, wave * RW, lane,
                                      tid, PT_ABL(a.ablate) & 1, sr);
   PT_TR(a, kind, 4);
   PT_TRW(a, kind, 16);
@@ -2225,7 +2312,7 @@ __device__ __forceinline__ void stag_wait(const int* cnt, int wave) {
 #define PT_FUSED_STAG_RA_FB 3
 #endif
 
-template <class S, int ACT, int HG, bool COH>
+template <class S, int ACT, int HG, bool COH, bool TL = false>
 __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvArgs<S>& c, int t, S* out_raw,
                                               const BnSlot& bnout, char* smem, int tid,
                                               const unsigned* wcnt = nullptr, unsigned wtarget = 0,
@@ -2248,13 +2335,18 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
   // and the rows it borrows are in, no workgroup barrier -- 65.5 -> 64.2 us;
   // fb 3 / 5: 55.4 -> 52.4 us, 4 / 4: 54.6: profiles/r05_libab_fused_stag*.txt)
   constexpr bool STAG = (PT_FUSED_STAG & 2) && (!COH || PT_PERSIST_STAG) && sizeof(S) == 2;
-  FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FA>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
+  // tiled frames (r06, TL): the unstaggered rows, then the border exchange
+  // (xb_exchange); separate instantiations, so the 32x32 kernels keep their
+  // registers (the exchange beside the staggered form spilled)
+  static_assert(!(TL && COH), "the persistent forward runs single-tile frames");
+  constexpr bool stag = STAG && !TL;
+  FaIn<S> nxt = fa_load(a, t, clip_off(b) + (size_t)(stag ? stag_row<PT_FUSED_STAG_RA_FA>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   // (r05) the finalising wave 7 stages no x: its BN loads and the others' x
   // loads are one HBM round trip each, side by side
   if (!(PT_ABL(a.ablate) & 131072) && (COH || wave < FUSED_NW - 1))
-    stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, COH ? CONV_NT : CONV_NT - 64, 1, 1);
-  if constexpr (STAG) {
+    stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, COH ? CONV_NT : CONV_NT - 64, TL ? a.ntx : 1, TL ? a.nty : 1);
+  if constexpr (stag) {
     int* cnt = L.cnt;
     if (tid < 8) cnt[tid] = 0;
     __syncthreads();
@@ -2292,11 +2384,11 @@ __device__ __forceinline__ void fused_fa_body(const CellArgs<S>& a, const ConvAr
                          (S*)L.tile);
   }
   PT_TR(a, PT_K_FUSED_FA, 3);
-  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FA);
+  fused_conv<S, false, TL>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FA, a.xflag);
   PT_TR(a, PT_K_FUSED_FA, 6);
 }
 
-template <class S, int ACT, int HG, bool COH>
+template <class S, int ACT, int HG, bool COH, bool TL = false>
 __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvArgs<S>& c, int t, S* out_raw,
                                               const BnSlot& bnout, char* smem, int tid,
                                               const unsigned* wcnt = nullptr, unsigned wtarget = 0,
@@ -2312,13 +2404,15 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
     bn_fwd_finalize<COH>(bnf_src(a, t, 0), bnf_nsrc(a), a.B * a.bn_world, a.eps, L.stat,
                          b == 0 ? a.bnstat + (size_t)t * 128 : nullptr, lane);
   constexpr bool STAG = (PT_FUSED_STAG & 1) && (!COH || PT_PERSIST_STAG) && sizeof(S) == 2;   // (bf16: the barrier-free conv form)
-  FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(STAG ? stag_row<PT_FUSED_STAG_RA_FB>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
+  static_assert(!(TL && COH), "the persistent forward runs single-tile frames");
+  constexpr bool stag = STAG && !TL;
+  FbIn<S> nxt = fb_load<S, HG>(a, t, clip_off(b) + (size_t)(stag ? stag_row<PT_FUSED_STAG_RA_FB>(wave, 0) : wave * FUSED_RW) * IMG * C, cl, h);
   tile_zero_halo<S, PADMAX, CONV_NT>((S*)L.tile, tid);   // rows fill the interior
   // (r05) the finalising wave 7 stages no x: its BN loads and the others' x
   // loads are one HBM round trip each, side by side
   if (!(PT_ABL(a.ablate) & 131072) && (COH || wave < FUSED_NW - 1))
-    stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, COH ? CONV_NT : CONV_NT - 64, 1, 1);
-  if constexpr (STAG) {
+    stage_x(a.x, a.xu8, L.xs, b, t, a.T, 0, IMG, tid, COH ? CONV_NT : CONV_NT - 64, TL ? a.ntx : 1, TL ? a.nty : 1);
+  if constexpr (stag) {
     int* cnt = L.cnt;
     if (tid < 8) cnt[tid] = 0;
     __syncthreads();
@@ -2360,19 +2454,20 @@ __device__ __forceinline__ void fused_fb_body(const CellArgs<S>& a, const ConvAr
                          (S*)L.tile);
   }
   PT_TR(a, PT_K_FUSED_FB, 3);
-  fused_conv<S>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FB);
+  fused_conv<S, false, TL>(a, c, out_raw, bnout, smem, L, b, wave, lane, tid, PT_K_FUSED_FB,
+                           a.xflag + a.B);
   PT_TR(a, PT_K_FUSED_FB, 6);
 }
 
-template <class S, int ACT, int HG>
+template <class S, int ACT, int HG, bool TL = false>
 __global__ __launch_bounds__(CONV_NT, 1) void k_fused_fa(CellArgs<S> a, ConvArgs<S> c) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  fused_fa_body<S, ACT, HG, false>(a, c, a.t, c.out_raw, c.bnout, smem, threadIdx.x);
+  fused_fa_body<S, ACT, HG, false, TL>(a, c, a.t, c.out_raw, c.bnout, smem, threadIdx.x);
 }
-template <class S, int ACT, int HG>
+template <class S, int ACT, int HG, bool TL = false>
 __global__ __launch_bounds__(CONV_NT, 1) void k_fused_fb(CellArgs<S> a, ConvArgs<S> c) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  fused_fb_body<S, ACT, HG, false>(a, c, a.t, c.out_raw, c.bnout, smem, threadIdx.x);
+  fused_fb_body<S, ACT, HG, false, TL>(a, c, a.t, c.out_raw, c.bnout, smem, threadIdx.x);
 }
 
 // Persistent forward (PT_CELL_PERSIST=1): the fused segments of all T frames
@@ -2651,8 +2746,10 @@ __global__ __launch_bounds__(PW_NT, 2) void k_conv_pw_ba(CellArgs<bf16_t> a, Con
     constexpr int RW = BAND_RW;
     const int lane = threadIdx.x & 63, h = lane >> 5, px = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if constexpr ((PT_PRIO & 64) != 0)        // the clip's part 1 lags: its conv beside part 0's rows
-      if (part == 1) __builtin_amdgcn_s_setprio(0); else __builtin_amdgcn_s_setprio(2);
+    if constexpr ((PT_PRIO & 64) != 0) {      // the clip's part 1 lags: its conv beside part 0's rows
+      if (part == 1) __builtin_amdgcn_s_setprio(0);
+      else __builtin_amdgcn_s_setprio(2);
+    }
     f32x16 acc[RW];
     bf16x4 p0[RW][4], p1[RW][4];
     const AddRowBand<RW> ar{(bf16_t*)c.out, (const bf16_t*)c.add0, (const bf16_t*)c.add1,
@@ -4456,6 +4553,7 @@ struct Plan {
   // workspace offsets
   size_t o_bnf_cnt, o_bnf_part, o_bnf_grp, o_bnb_cnt, o_bnb_part, o_bnb_grp;   // BnSlot storage
   size_t o_bnf_done, o_err;   // persistent forward: group-sum counters [T][2], give-up flag
+  size_t o_xflag;             // fused tiled forward: border flags [2][B] (xb_exchange)
   size_t bnf_cnt_bytes, bnb_cnt_bytes;
   size_t o_tr[NTRANS], o_dci, o_dce, o_slab, o_wslab, ws;
   int nwg;
@@ -4514,6 +4612,7 @@ Plan plan(const pt_cell_desc* d) {
   p.o_bnf_cnt = o; o += al((size_t)p.T * 2 * NGRP * 4);
   p.o_bnf_done = o; o += al((size_t)p.T * 2 * 4);
   p.o_err = o; o += al(4);
+  p.o_xflag = o; o += al((size_t)2 * p.B * 4);
   p.o_bnf_grp = o; o += al((size_t)p.T * 2 * NGRP * 96 * 8);
   p.bnf_cnt_bytes = PT_BN_MODE == 0 ? o - p.o_bnf_cnt : p.o_bnf_grp - p.o_bnf_cnt;
   p.o_bnf_part = o; o += al((size_t)p.T * 2 * p.B * 64 * 4);
@@ -4586,6 +4685,10 @@ void fill_args(CellArgs<S>& a, const pt_cell_desc* d, const Plan& p, const void*
     a.GEfin = (const float*)(ws + p.o_tr[NTRANS - 1]);
     a.dci_s = (S*)(ws + p.o_dci); a.dce_s = (S*)(ws + p.o_dce);
     a.slab = (float*)(ws + p.o_slab);
+    // (the forward has no backward transients live: the border slots use dEn's)
+    a.xch = (S*)(ws + p.o_tr[0]);
+    a.xflag = (unsigned*)(ws + p.o_xflag);
+    a.xerr = (unsigned*)(ws + p.o_err);
   }
 }
 
@@ -4614,11 +4717,14 @@ template <class K, class A, class Cv>
 void launch_fused(K kern, int nclip, size_t lds, hipStream_t st, const A& a, const Cv& c) {
   hipLaunchKernelGGL(kern, dim3(nclip), dim3(CONV_NT), lds, st, a, c);
 }
-#define FUSED_LAUNCH(kern, c)                                                                \
-  (a.hgru ? (a.act ? launch_fused(kern<S, 1, 1>, p.B, fused_lds_bytes<S>(), st, a, c)         \
-                   : launch_fused(kern<S, 0, 1>, p.B, fused_lds_bytes<S>(), st, a, c))        \
-          : (a.act ? launch_fused(kern<S, 1, 0>, p.B, fused_lds_bytes<S>(), st, a, c)         \
-                   : launch_fused(kern<S, 0, 0>, p.B, fused_lds_bytes<S>(), st, a, c)))
+#define FUSED_LAUNCH_TL(kern, c, TL)                                                                \
+  (a.hgru ? (a.act ? launch_fused(kern<S, 1, 1, TL>, p.B, fused_lds_bytes<S>(), st, a, c)             \
+                   : launch_fused(kern<S, 0, 1, TL>, p.B, fused_lds_bytes<S>(), st, a, c))            \
+          : (a.act ? launch_fused(kern<S, 1, 0, TL>, p.B, fused_lds_bytes<S>(), st, a, c)             \
+                   : launch_fused(kern<S, 0, 0, TL>, p.B, fused_lds_bytes<S>(), st, a, c)))
+// tiled frames: the border-exchange instantiations (xb_exchange)
+#define FUSED_LAUNCH(kern, c) \
+  (p.ntx * p.nty > 1 ? FUSED_LAUNCH_TL(kern, c, true) : FUSED_LAUNCH_TL(kern, c, false))
 
 #define SETLDS(kern, bytes) \
   HIPCHK(hipFuncSetAttribute((const void*)(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (bytes)))
@@ -4662,13 +4768,21 @@ int set_lds_attrs() {
   SETLDS((k_pw_ba2<S, 1, 0>), (pa2_lds_bytes<S>()));
   SETLDS((k_pw_ba2<S, 1, 1>), (pa2_lds_bytes<S>()));
   SETLDS((k_fused_fa<S, 0, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fa<S, 0, 0, true>), fused_lds_bytes<S>());
   SETLDS((k_fused_fa<S, 0, 1>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fa<S, 0, 1, true>), fused_lds_bytes<S>());
   SETLDS((k_fused_fa<S, 1, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fa<S, 1, 0, true>), fused_lds_bytes<S>());
   SETLDS((k_fused_fa<S, 1, 1>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fa<S, 1, 1, true>), fused_lds_bytes<S>());
   SETLDS((k_fused_fb<S, 0, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 0, 0, true>), fused_lds_bytes<S>());
   SETLDS((k_fused_fb<S, 0, 1>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 0, 1, true>), fused_lds_bytes<S>());
   SETLDS((k_fused_fb<S, 1, 0>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 1, 0, true>), fused_lds_bytes<S>());
   SETLDS((k_fused_fb<S, 1, 1>), fused_lds_bytes<S>());
+  SETLDS((k_fused_fb<S, 1, 1, true>), fused_lds_bytes<S>());
   SETLDS((k_persist_fwd<S, 0, 0>), fused_lds_bytes<S>());
   SETLDS((k_persist_fwd<S, 0, 1>), fused_lds_bytes<S>());
   SETLDS((k_persist_fwd<S, 1, 0>), fused_lds_bytes<S>());
@@ -4780,8 +4894,20 @@ bool pwa2_env() { return PT_SW("PT_PWA2", PT_PWA2_DEF) == 1; }
 bool wg16_env() { return PT_SW("PT_WG16", 1) != 0; }
 // its LDS-DMA band staging on untiled frames (PT_WGDMA=0: register staging)
 bool wgdma_env() { return PT_SW("PT_WGDMA", 1) != 0; }
+// r06: tiled frames through the fused segments too (the border exchange,
+// xb_exchange; opt-in, PT_FUSED_TILED=1 in diag builds): bitwise the split
+// forward, but at cfg4 (B = 128 clips of 2 x 2 tiles) k_fused_fa / fb take
+// 135.4 / 114.3 us per frame against 76.4 + 55.9 / 57.1 + 56.0 us split
+// (86.70 vs 87.06 ms per step, profiles/r06_libab_fused_tiled.txt): its
+// 146 KB of LDS holds one workgroup per CU, so 512 tile workgroups run in two
+// rounds, each as long as the 32x32 launch plus the exchange, while the split
+// point-wise kernels run four workgroups per CU
+#ifndef PT_FUSED_TILED_DEF
+#define PT_FUSED_TILED_DEF 0
+#endif
+bool fused_tiled_env() { return PT_SW("PT_FUSED_TILED", PT_FUSED_TILED_DEF) != 0; }
 bool use_fused(const pt_cell_desc* d, const Plan& p) {
-  return fused_env() && d->dtype == PT_DTYPE_BF16 && p.ntx * p.nty == 1 &&
+  return fused_env() && d->dtype == PT_DTYPE_BF16 && (p.ntx * p.nty == 1 || fused_tiled_env()) &&
          p.K <= 2 * PADMAX + 1 && !d->no_inh;
 }
 
@@ -4852,7 +4978,7 @@ int run_forward(const pt_cell_desc* d, const void* x, const pt_cell_params* pr, 
   ConvArgs<S> ca = conv_args(a), cb = conv_args(a);
   ca.wf = a.wf_inh;
   cb.wf = a.wf_exc;
-  if (use_fused(d, p) && !syncbn(dist) && persist_env() && persist_fits<S>(p.B)) {
+  if (use_fused(d, p) && p.ntx * p.nty == 1 && !syncbn(dist) && persist_env() && persist_fits<S>(p.B)) {
     // it reads its give-up flag back (a host sync below): illegal under an
     // outer stream capture, so refuse that case with a clear message
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -5148,7 +5274,7 @@ int pt_cell_forward_dist(const pt_cell_desc* d, const void* x, const pt_cell_par
   if (int rc = bf ? set_lds_attrs<bf16_t>() : set_lds_attrs<float>()) return rc;
   ptg::Key k;
   k.add(*d).add(x).add(*p).add(saved).add(ws).add(e_last).add(gates).add(ablate_env())
-      .add(fused_env())
+      .add(fused_env()).add(fused_tiled_env())
       .add(persist_env()).add(xmap_env());
   return g_graphs.run(k.b.data(), k.b.size(), st, PT_ERR_HIP, body);
 }

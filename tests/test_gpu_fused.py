@@ -30,9 +30,9 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _run(m, x, y, fused, persist=False, band=False, cpa=1, band2_tiled=1):
+def _run(m, x, y, fused, persist=False, band=False, cpa=1, band2_tiled=1, fused_tiled=0):
     with variants(PT_CELL_FUSED=int(fused), PT_CELL_PERSIST=int(persist), PT_CONV_BAND=int(band),
-                  PT_CPA=int(cpa), PT_BAND2_TILED=int(band2_tiled)):
+                  PT_CPA=int(cpa), PT_BAND2_TILED=int(band2_tiled), PT_FUSED_TILED=int(fused_tiled)):
         m.zero_grad(set_to_none=True)
         out, _ = m(x)
         F.binary_cross_entropy_with_logits(out, y.reshape(-1, 1)).backward()
@@ -107,6 +107,41 @@ def test_staggered_two_band_conv_on_tiled_frames_is_bitwise_the_whole_clip_conv(
     o0, s0, g0, gr0 = _run(m, x, y, fused=True, band=3, band2_tiled=1, cpa=cpa)
     assert torch.isfinite(o1).all()
     assert torch.equal(o1, o0), (o1 - o0).abs().max().item()
+    bad = {k: ((gr1[k] - gr0[k]).abs().max() / gr0[k].abs().max().clamp_min(1e-30)).item()
+           for k in gr0 if k.startswith(("unit1.", "preproc.")) and not torch.equal(gr1[k], gr0[k])}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("cell,h,w,b,t", [("hgru", 64, 64, 4, 6), ("hgru", 96, 96, 2, 4), ("int", 64, 96, 3, 5),
+                                          ("hgru", 64, 64, 128, 8)])
+def test_fused_forward_on_tiled_frames_is_bitwise_the_split_forward(cell, h, w, b, t):
+    """k_fused_fa / k_fused_fb on frames of several 32x32 tiles (r06, opt-in
+    PT_FUSED_TILED=1: each tile workgroup publishes its conv input's border
+    and takes its halo from the neighbouring tiles' workgroups of the same
+    launch, xb_exchange) against the split forward (k_pw_fa, k_conv_fwd with
+    tile_halo, ...): logits, per-frame states and gates, every gradient; the
+    3x3-tile frame's middle tile has all 8 neighbours, and (128, 64x64) is
+    cfg4's launch of 512 tile workgroups."""
+    from models import InT, ffhgru_hierarchy as hg
+    dev = _dev()
+    torch.manual_seed(h + w + b)
+    m = (hg.FFhGRU(dimensions=32, timesteps=t, kernel_size=7) if cell == "hgru"
+         else InT.InT(dimensions=32, timesteps=t, kernel_size=7))
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
+                p.uniform_(0.5, 1.5)
+            elif n.endswith(("mu", "gamma")):
+                p.uniform_(-0.5, 0.5)
+    m = m.to(dev)
+    m.cell_dtype = "bf16"
+    x = torch.rand(b, 3, t, h, w, device=dev)
+    y = (torch.arange(b, device=dev) % 2).float()
+    o1, s1, g1, gr1 = _run(m, x, y, fused=True, fused_tiled=1)
+    o0, s0, g0, gr0 = _run(m, x, y, fused=True, fused_tiled=0)
+    assert torch.isfinite(o1).all() and torch.isfinite(s1).all()
+    for name, u, v in (("logits", o1, o0), ("states", s1, s0), ("gates", g1, g0)):
+        assert torch.equal(u, v), (name, (u - v).abs().max().item(), (u != v).sum().item())
     bad = {k: ((gr1[k] - gr0[k]).abs().max() / gr0[k].abs().max().clamp_min(1e-30)).item()
            for k in gr0 if k.startswith(("unit1.", "preproc.")) and not torch.equal(gr1[k], gr0[k])}
     assert not bad, bad

@@ -48,7 +48,8 @@ def _setup():
 # and the kernel-variant A/B switches)
 NON_DEFAULT = dict(PT_CELL_ABLATE=str(1 | 4 | 8 | 32 | 512), PT_CELL_DEBUG_STOP="2",
                    PT_CELL_FUSED="0", PT_PWB2="0", PT_PWA2="1", PT_WG16="0", PT_WGDMA="0",
-                   PT_CELL_PERSIST="1", PT_XCD_MAP="0", PT_CONV_BAND="0", PT_CPA="0", PT_BAND2_TILED="0")
+                   PT_CELL_PERSIST="1", PT_XCD_MAP="0", PT_CONV_BAND="0", PT_CPA="0", PT_BAND2_TILED="0",
+                   PT_FUSED_TILED="1")
 
 
 def test_release_library_ignores_the_diagnostic_switches():

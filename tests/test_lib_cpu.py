@@ -293,7 +293,8 @@ def test_release_library_has_no_diagnostic_switches():
 # the kernel-variant switches (PT_SW, csrc/pt_device.h): A/B experiments of
 # DESIGN.md §9, read only by the diagnostic builds
 CELL_SWITCHES = (b"PT_CELL_FUSED", b"PT_PWB2", b"PT_PWA2", b"PT_WG16", b"PT_WGDMA", b"PT_CELL_PERSIST",
-                 b"PT_XCD_MAP", b"PT_CONV_BAND", b"PT_CPA", b"PT_BAND2_TILED")
+                 b"PT_XCD_MAP", b"PT_CONV_BAND", b"PT_CPA", b"PT_BAND2_TILED",
+                 b"PT_FUSED_TILED")
 LSTM_SWITCHES = (b"PT_LCONV_FAST", b"PT_LCONVT8", b"PT_LWGRAD2", b"PT_LPW_FUSE")
 
 

@@ -6,7 +6,8 @@ the model's calls to it) and runs the same forward + backward, interleaved
 round by round (cdna_hip_programming.md §5.4 rule 24: compare on one box, in
 one process); per-kind average launch times from each library's own launch
 events (pt_cell_timing_*) and the summed device ms per step, medians over the
-rounds.  B, T, DT as tools/ablate.py."""
+rounds.  B, T, DT as tools/ablate.py; CELL=hgru with HW=64 runs cfg4's FFhGRU
+on 64x64 frames (tiled)."""
 import glob
 import os
 import sys
@@ -17,7 +18,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "pathtracker-models_amd")]
 import torch  # noqa: E402
 
 from ptamd import _lib  # noqa: E402
-from models import InT as int_mod  # noqa: E402
+from models import InT as int_mod, ffhgru_hierarchy as hg  # noqa: E402
 
 
 def main():
@@ -30,9 +31,13 @@ def main():
         glob.glob(os.path.join(REPO, "pathtracker-models_amd", "ptamd", "ab", "*.so")))
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    m = int_mod.InT(dimensions=32, timesteps=t, kernel_size=7).to(dev)
+    hw = int(os.environ.get("HW", 32))
+    if os.environ.get("CELL", "int") == "hgru":
+        m = hg.FFhGRU(dimensions=32, timesteps=t, kernel_size=7).to(dev)
+    else:
+        m = int_mod.InT(dimensions=32, timesteps=t, kernel_size=7).to(dev)
     m.cell_dtype = dtype
-    x = torch.rand(b, 3, t, 32, 32, device=dev)
+    x = torch.rand(b, 3, t, hw, hw, device=dev)
     kinds = [k for k in _lib.KIND_NAMES if k not in ("k_prep", "k_reduce")]
     res = {p: {k: [] for k in kinds} for p in libs}
     tot = {p: [] for p in libs}
