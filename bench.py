@@ -329,6 +329,10 @@ def main():
     ap.add_argument("--no-grad-overlap", action="store_true",
                     help="N>1: all-reduce every gradient after backward (default: the cell's "
                          "early gradients on a side stream under the k x k weight-gradient kernel)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N>1 on a ONE-GPU box: every rank on cuda:0, gloo instead of RCCL -- "
+                         "exercises the multi-rank step (broadcast, the three-part gradient "
+                         "exchange, the MAX over ranks); not a measurement")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check on CPU (gloo), no GPU work")
     args = ap.parse_args()
@@ -347,9 +351,14 @@ def main():
     from ptamd import _lib
     from models import InT as int_mod
 
+    if args.rehearse:
+        local_rank = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        assert dist.get_world_size() == args.gpus and dist.get_backend() == "nccl"
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            assert dist.get_world_size() == args.gpus and dist.get_backend() == "nccl"
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -505,6 +514,8 @@ def main():
         }
         if f32 is not None:
             line["f32_cell"] = f32
+        if args.rehearse:
+            line["rehearsal"] = "all ranks on one GPU over gloo: a path check, not a measurement"
         if not np.isfinite(line["loss"]):
             print("bench.py: WARNING non-finite training loss", file=sys.stderr, flush=True)
         if world == 1 and not args.no_cpu_baseline:
