@@ -153,6 +153,24 @@ struct LConvArgs {
 // their own fragment sets -- the per-step x-conv and h-conv of the clip
 // ConvLSTM in ONE launch, P_t = Wx x_t + Wh h_{t-1} + b, instead of an
 // all-steps x-conv whose P_t the h-conv then read back and rewrote.
+// Issue priority by progress (r06, PT_LPRIO; the cell library's PT_PRIO 4):
+// two workgroups share a CU and at equal priority the SIMD arbiter prefers the
+// older wave, so the first one runs ahead and the second finishes alone; a
+// workgroup lowers its priority as it progresses (3 at the start, 0 in the
+// last quarter).  bit 0: k_lconv (kernel columns), bit 1: k_lwgrad (units).
+#ifndef PT_LPRIO
+#define PT_LPRIO 0
+#endif
+__device__ __forceinline__ void lprio(int done, int total) {
+  const int q = total > 0 ? 3 - (4 * done) / total : 0;
+  switch (q < 0 ? 0 : q) {
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+  }
+}
+
 template <class S, int K, int NI, int NO, int NTH = NT, bool DUAL = false>
 __global__ __launch_bounds__(NTH, (conv_occ<S, K, NO>())) void k_lconv(LConvArgs a) {
   static_assert(!DUAL || NI == 2, "DUAL: two input groups");
@@ -299,6 +317,7 @@ __global__ __launch_bounds__(NTH, (conv_occ<S, K, NO>())) void k_lconv(LConvArgs
     if (!DUAL && TPF && ig + 1 < NI) ld_tile(ig + 1, v);
 #pragma unroll 1
     for (int kw = 0; kw < K; ++kw) {
+      if constexpr ((PT_LPRIO & 1) != 0) lprio(ig * K + kw, NI * K);
       const S* tl = DUAL && ig ? tile + L::BYTES / sizeof(S) : tile;
       // (after the last column: a harmless reload of group 0's first column)
       const F* wkn = kw + 1 < K ? gwf(ig) + (size_t)(kw + 1) * TT::KS * 64 + lane
@@ -734,6 +753,7 @@ __global__ __launch_bounds__(NT, 1) void k_lwgrad(LWgradArgs a) {
   }
   __syncthreads();
   for (int u = 0; u < nunits; ++u) {
+    if constexpr ((PT_LPRIO & 2) != 0) lprio(u, nunits);
     const S* xt = buf + (u & 1) * Bd::BE;
     const S* dt = xt + Bd::XE;
     const bool more = u + 1 < nunits;
