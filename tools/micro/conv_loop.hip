@@ -6,6 +6,10 @@
 // at the issue bound).  Reports shader cycles per MFMA per SIMD (s_memtime
 // around the loop, wave 0 of every workgroup) for 4 waves per workgroup (one
 // per SIMD, the band-1 conv's situation) and 8 (two per SIMD).
+// -DRANDOM_DATA (r06): the tile and the weights hold pseudo-random bf16 values
+// in [-1, 1) instead of constants (MFMA power depends on the operand bits),
+// and each configuration also runs 200 launches back to back (sustained
+// clock).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize
 //        -I include -I pathtracker-models_amd/csrc tools/micro/conv_loop.hip
 #include <hip/hip_runtime.h>
@@ -32,7 +36,16 @@ __global__ __launch_bounds__(NW * 64, 1) void k_loop(const Tr<bf16_t>::frag* __r
   bf16_t* tile = (bf16_t*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef RANDOM_DATA
+  for (int i = tid; i < 22 * TILE * C / 2; i += NW * 64) {   // 2 bf16 per word, [-1, 1)
+    unsigned x = (unsigned)(i * 2654435761u) ^ (blockIdx.x * 40503u);
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    const unsigned lo = 0x3f80u | (x & 0x807fu), hi = 0x3f80u | ((x >> 16) & 0x807fu);
+    ((unsigned*)tile)[i] = (lo & 0xbfffu) | ((hi & 0xbfffu) << 16);
+  }
+#else
   for (int i = tid; i < 22 * TILE * C / 8; i += NW * 64) ((uint4*)tile)[i] = make_uint4(0x3f803f80u, 0, 0x3f80u, 0);
+#endif
   __syncthreads();
   f32x16 acc[4];
 #pragma unroll
@@ -57,7 +70,14 @@ void run(const Tr<bf16_t>::frag* wf, float* out, unsigned long long* cyc, int gr
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  const int R = 20;
+#ifndef REPS
+#ifdef RANDOM_DATA
+#define REPS 200
+#else
+#define REPS 20
+#endif
+#endif
+  const int R = REPS;
   hipEventRecord(a, 0);
   for (int r = 0; r < R; ++r) hipLaunchKernelGGL(k_loop<NW>, dim3(grid), dim3(NW * 64), lds, 0, wf, out, cyc);
   hipEventRecord(b, 0);
@@ -80,6 +100,17 @@ int main() {
   const size_t nfr = 49 * 2 * 64;
   hipMalloc(&wf, nfr * sizeof(Tr<bf16_t>::frag));
   hipMemset(wf, 0, nfr * sizeof(Tr<bf16_t>::frag));
+#ifdef RANDOM_DATA
+  {
+    std::vector<unsigned short> hw(nfr * sizeof(Tr<bf16_t>::frag) / 2);
+    unsigned x = 12345u;
+    for (auto& v : hw) {
+      x = x * 1664525u + 1013904223u;
+      v = (unsigned short)(0x3c00u | ((x >> 9) & 0x80ffu));   // |w| in [2^-7, 2^-6), either sign
+    }
+    hipMemcpy(wf, hw.data(), hw.size() * 2, hipMemcpyHostToDevice);
+  }
+#endif
   float* out;
   hipMalloc(&out, 256 * 512 * 4);
   unsigned long long* cyc;
