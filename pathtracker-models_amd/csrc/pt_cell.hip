@@ -1349,6 +1349,13 @@ __device__ __forceinline__ void prio_by_step(int step) {   // 3 - step, clamped;
 }
 // -------------------------------------------------------------------------
 constexpr int BAND_ROWS = 16, BAND_NT = 256, BAND_TR = BAND_ROWS + 2 * PADMAX;
+// r06: k_conv_bwd_band2's first fill loads issued before the BatchNorm table
+// (band_fill_pre): bitwise, measured no faster (conv_bb 36.9 vs 36.6 us, the
+// step 20.764 ms both, profiles/r06_libab_fillpre.txt -- the fill is bound by
+// the launch's HBM burst, not by the table's latency); off by default
+#ifndef PT_FILL_PRE
+#define PT_FILL_PRE 0
+#endif
 constexpr int band_tile_bytes() { return BAND_TR * TILE * C * 2; }
 
 template <int RW>
@@ -1456,6 +1463,94 @@ __device__ __forceinline__ void band_halo(const ConvArgs<bf16_t>& a, const float
   }
 }
 
+// One band's BatchNorm-backward fill (r05; the tile rows [y0 - PAD, y0 + 16 +
+// PAD) within the image, each pixel of the band's own rows also written out).
+// r06: the first batch of each thread's loads can be issued before the
+// BatchNorm table exists (FillPre, band_fill_pre: the loads do not need it),
+// so their HBM latency runs under the table's group-sum loads instead of
+// after the barrier that publishes it -- by every wave but wave 0, which
+// computes the table (vmcnt counts in order: its group-sum loads would wait
+// behind the fill's).  Same values, same arithmetic.
+constexpr int BFILL_BATCH = 4;
+struct FillPre { u32x4 dv[BFILL_BATCH], rv[BFILL_BATCH]; };
+__device__ __forceinline__ int band_fill_n(int y0) {
+  const int r0 = y0 - PADMAX < 0 ? 0 : y0 - PADMAX;
+  const int r1 = y0 + BAND_ROWS + PADMAX > IMG ? IMG : y0 + BAND_ROWS + PADMAX;
+  return (r1 - r0) * IMG * (C / 8);
+}
+template <int NTH>
+__device__ __forceinline__ void band_fill_ld(const ConvArgs<bf16_t>& a, size_t cb, int y0, int i0, int n,
+                                             u32x4 (&dv)[BFILL_BATCH], u32x4 (&rv)[BFILL_BATCH]) {
+  constexpr int NCH = C / 8;
+  const int r0 = y0 - PADMAX < 0 ? 0 : y0 - PADMAX;
+#pragma unroll
+  for (int k = 0; k < BFILL_BATCH; ++k) {
+    const int idx = i0 + k * NTH < n ? i0 + k * NTH : i0;
+    const int pix = r0 * IMG + idx / NCH, q = idx % NCH;
+    const size_t e = cb + (size_t)pix * C + q * 8;
+#if PT_BAND_XNOFILL     // (timing experiments only: no fill loads)
+    dv[k] = u32x4{(unsigned)e, 0u, 0u, 0u}; rv[k] = dv[k];
+#else
+    dv[k] = *(const u32x4*)(a.dc + e);
+    rv[k] = *(const u32x4*)(a.raw + e);
+#endif
+  }
+}
+template <int NTH>
+__device__ __forceinline__ void band_fill_pre(const ConvArgs<bf16_t>& a, size_t cb, int y0, int tid, FillPre& p) {
+  band_fill_ld<NTH>(a, cb, y0, tid, band_fill_n(y0), p.dv, p.rv);
+}
+template <int NTH>
+__device__ __forceinline__ void band_fill_st(const ConvArgs<bf16_t>& a, const float* tbl, bf16_t* tile,
+                                             size_t cb, int y0, int i0, int n,
+                                             const u32x4 (&dv)[BFILL_BATCH], const u32x4 (&rv)[BFILL_BATCH]) {
+  using S = bf16_t;
+  constexpr int CPB = 8, NCH = C / CPB;
+  const int r0 = y0 - PADMAX < 0 ? 0 : y0 - PADMAX;
+#pragma unroll
+  for (int k = 0; k < BFILL_BATCH; ++k) {
+    const int idx = i0 + k * NTH;
+    if (idx >= n) break;
+    const int pix = r0 * IMG + idx / NCH, q = idx % NCH, ch0 = q * CPB;
+    const S* rr = (const S*)&rv[k];
+    const S* dd = (const S*)&dv[k];
+    uint4 ov;
+    S* oo = (S*)&ov;
+#pragma unroll
+    for (int j = 0; j < CPB; ++j) {
+      const int ch = ch0 + j;
+      oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
+    }
+    const int y = pix >> 5, x = pix & 31;
+    if (y >= y0 && y < y0 + BAND_ROWS)          // each pixel written out by one band
+      *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
+    *(uint4*)(tile + tile_off<S, PADMAX>(y - y0 + PADMAX, x + PADMAX, ch0)) = ov;
+  }
+}
+template <int NTH, bool PRE = false>
+__device__ __forceinline__ void band_fill(const ConvArgs<bf16_t>& a, const float* tbl, bf16_t* tile,
+                                          size_t cb, int y0, int tid, const FillPre& pre = FillPre{},
+                                          bool use_pre = false) {
+  const int n = band_fill_n(y0);
+  int i0 = tid;
+  if constexpr (PRE) {          // the first batch: prefetched (use_pre) or loaded here
+    u32x4 dv[BFILL_BATCH], rv[BFILL_BATCH];
+    if (use_pre) {
+#pragma unroll
+      for (int k = 0; k < BFILL_BATCH; ++k) { dv[k] = pre.dv[k]; rv[k] = pre.rv[k]; }
+    } else {
+      band_fill_ld<NTH>(a, cb, y0, i0, n, dv, rv);
+    }
+    if (i0 < n) band_fill_st<NTH>(a, tbl, tile, cb, y0, i0, n, dv, rv);
+    i0 += BFILL_BATCH * NTH;
+  }
+  for (; i0 < n; i0 += BFILL_BATCH * NTH) {
+    u32x4 dv[BFILL_BATCH], rv[BFILL_BATCH];
+    band_fill_ld<NTH>(a, cb, y0, i0, n, dv, rv);
+    band_fill_st<NTH>(a, tbl, tile, cb, y0, i0, n, dv, rv);
+  }
+}
+
 // The band's conv with a row hook (hook(i, acc): output row i finished;
 // k_conv_bwd_band adds the addends and stores, k_conv_pw_ba keeps the row).
 constexpr int BAND_RW = BAND_ROWS / (BAND_NT / 64);
@@ -1485,47 +1580,10 @@ __device__ __forceinline__ void band_conv_body(const ConvArgs<bf16_t>& a, char* 
     uint4* z = (uint4*)tile;
     for (int i = tid; i < band_tile_bytes() / 16; i += BAND_NT) z[i] = make_uint4(0, 0, 0, 0);
   }
-  // image rows of the band's tile: [y0 - PAD, y0 + 16 + PAD) within the image
-  const int r0 = y0 - PADMAX < 0 ? 0 : y0 - PADMAX;
-  const int r1 = y0 + BAND_ROWS + PADMAX > IMG ? IMG : y0 + BAND_ROWS + PADMAX;
   auto fill = [&](int) {
-    constexpr int CPB = 8, NCH = C / CPB;
-    const int n = (r1 - r0) * IMG * NCH;
-    constexpr int BATCH = 4;
-    for (int i0 = tid; i0 < n; i0 += BATCH * BAND_NT) {
-      uint4 dv[BATCH], rv[BATCH];
-#pragma unroll
-      for (int k = 0; k < BATCH; ++k) {
-        const int idx = i0 + k * BAND_NT < n ? i0 + k * BAND_NT : i0;
-        const int pix = r0 * IMG + idx / NCH, q = idx % NCH;
-        const size_t e = cb + (size_t)pix * C + q * CPB;
-#if PT_BAND_XNOFILL     // (timing experiments only: no fill loads)
-        dv[k] = make_uint4(e, 0, 0, 0); rv[k] = dv[k];
-#else
-        dv[k] = *(const uint4*)(a.dc + e);
-        rv[k] = *(const uint4*)(a.raw + e);
-#endif
-      }
-#pragma unroll
-      for (int k = 0; k < BATCH; ++k) {
-        const int idx = i0 + k * BAND_NT;
-        if (idx >= n) break;
-        const int pix = r0 * IMG + idx / NCH, q = idx % NCH, ch0 = q * CPB;
-        const S* rr = (const S*)&rv[k];
-        const S* dd = (const S*)&dv[k];
-        uint4 ov;
-        S* oo = (S*)&ov;
-#pragma unroll
-        for (int j = 0; j < CPB; ++j) {
-          const int ch = ch0 + j;
-          oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
-        }
-        const int y = pix >> 5, x = pix & 31;
-        if (y >= y0 && y < y0 + BAND_ROWS)          // each pixel written out by one band
-          *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
-        *(uint4*)(tile + tile_off<S, PADMAX>(y - y0 + PADMAX, x + PADMAX, ch0)) = ov;
-      }
-    }
+    // (no prefetch here: beside the first weight column and the hook's addend
+    // registers it spilled in k_conv_pw_ba)
+    band_fill<BAND_NT>(a, tbl, tile, cb, y0, tid);
     if (a.ntx * a.nty > 1) band_halo<BAND_NT>(a, tbl, tile, b, band, tid);   // tiled frames (r06)
   };
 #pragma unroll
@@ -1559,47 +1617,6 @@ __global__ __launch_bounds__(BAND_NT, 2) void k_conv_bwd_band(ConvArgs<bf16_t> a
 constexpr int BAND2_NT = 512;
 constexpr int band2_lds_bytes() { return 2 * band_tile_bytes() + CONV_MISC * 4; }
 
-template <int NTH>
-__device__ __forceinline__ void band_fill(const ConvArgs<bf16_t>& a, const float* tbl, bf16_t* tile,
-                                          size_t cb, int y0, int tid) {
-  using S = bf16_t;
-  const int r0 = y0 - PADMAX < 0 ? 0 : y0 - PADMAX;
-  const int r1 = y0 + BAND_ROWS + PADMAX > IMG ? IMG : y0 + BAND_ROWS + PADMAX;
-  constexpr int CPB = 8, NCH = C / CPB;
-  const int n = (r1 - r0) * IMG * NCH;
-  constexpr int BATCH = 4;
-  for (int i0 = tid; i0 < n; i0 += BATCH * NTH) {
-    uint4 dv[BATCH], rv[BATCH];
-#pragma unroll
-    for (int k = 0; k < BATCH; ++k) {
-      const int idx = i0 + k * NTH < n ? i0 + k * NTH : i0;
-      const int pix = r0 * IMG + idx / NCH, q = idx % NCH;
-      const size_t e = cb + (size_t)pix * C + q * CPB;
-      dv[k] = *(const uint4*)(a.dc + e);
-      rv[k] = *(const uint4*)(a.raw + e);
-    }
-#pragma unroll
-    for (int k = 0; k < BATCH; ++k) {
-      const int idx = i0 + k * NTH;
-      if (idx >= n) break;
-      const int pix = r0 * IMG + idx / NCH, q = idx % NCH, ch0 = q * CPB;
-      const S* rr = (const S*)&rv[k];
-      const S* dd = (const S*)&dv[k];
-      uint4 ov;
-      S* oo = (S*)&ov;
-#pragma unroll
-      for (int j = 0; j < CPB; ++j) {
-        const int ch = ch0 + j;
-        oo[j] = (S)(tbl[ch] * ldf(dd + j) + tbl[32 + ch] * ldf(rr + j) + tbl[64 + ch]);
-      }
-      const int y = pix >> 5, x = pix & 31;
-      if (y >= y0 && y < y0 + BAND_ROWS)          // each pixel written out by one band
-        *(uint4*)(a.fill_out + cb + (size_t)pix * C + ch0) = ov;
-      *(uint4*)(tile + tile_off<S, PADMAX>(y - y0 + PADMAX, x + PADMAX, ch0)) = ov;
-    }
-  }
-}
-
 __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t> a) {
   using S = bf16_t;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1613,6 +1630,9 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
   const int b = blockIdx.x;
   const size_t cb = clip_off(b);
   PT_TR(a, a.trace_kind, 0);
+  FillPre pre;
+  const bool use_pre = PT_FILL_PRE != 0 && tid >= 64;    // (wave 0 computes the table)
+  if (use_pre) band_fill_pre<BAND2_NT>(a, cb, 0, tid, pre);   // under the table's loads
   if (tid < 32) {     // BN backward as an affine map per channel (as conv_body)
     const double inv = 1.0 / ((double)a.bnB * NPIX);
     double sd = 0.0, sdx = 0.0;
@@ -1631,7 +1651,7 @@ __global__ __launch_bounds__(BAND2_NT, 1) void k_conv_bwd_band2(ConvArgs<bf16_t>
   }
   __syncthreads();
   PT_TR(a, a.trace_kind, 1);
-  band_fill<BAND2_NT>(a, tbl, tile0, cb, 0, tid);
+  band_fill<BAND2_NT, PT_FILL_PRE != 0>(a, tbl, tile0, cb, 0, tid, pre, use_pre);
   const bool tiled = a.ntx * a.nty > 1;
   if (tiled) band_halo<BAND2_NT>(a, tbl, tile0, b, 0, tid);
   __syncthreads();
