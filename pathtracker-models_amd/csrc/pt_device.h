@@ -727,8 +727,19 @@ __device__ __forceinline__ void conv_run_k(f32x16 (&acc)[RW], Fill& fill,
         for (int s = 0; s < KSP; ++s) bw[0][kd][s] = wf[((kd * K + kw + 1) * TT::KS + s) * 64 + lane];
       }
       if constexpr (Done::active && RowPreLead<Done>::v > 0 && kw == K - 1) {
-        constexpr int ip = tr - (K - 1) + RowPreLead<Done>::v;
-        if constexpr (ip >= 0 && ip < RW) row_pre(done, ip);
+        // row i's pre-load at step tr = i + K - 1 - lead of the last column,
+        // or at its first step when that is earlier (k < lead + 2: without
+        // the clamp rows 0 .. lead - k + 1 never had their addends loaded)
+        constexpr int L = RowPreLead<Done>::v;
+        if constexpr (tr == 0) {
+          static_for<0, RW>([&](auto c) {
+            constexpr int i = decltype(c)::value;
+            if constexpr (i + K - 1 - L <= 0) row_pre(done, i);
+          });
+        } else {
+          constexpr int ip = tr - (K - 1) + L;
+          if constexpr (ip >= 0 && ip < RW) row_pre(done, ip);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (Done::active && kw == K - 1 && tr >= K - 1 && tr - (K - 1) < RW)
