@@ -26,9 +26,9 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _perturbed(cls, t, seed, **kw):
+def _perturbed(cls, t, seed, k=7, **kw):
     torch.manual_seed(seed)
-    m = cls(dimensions=32, timesteps=t, kernel_size=7, **kw)
+    m = cls(dimensions=32, timesteps=t, kernel_size=k, **kw)
     with torch.no_grad():
         for n, p in m.named_parameters():
             if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
@@ -65,6 +65,65 @@ def _batch(seed, b, t, hw=32):
     clips, labels = synth.make_batch(seed, b, t, h=hw, w=hw)
     x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float()
     return x, torch.tensor([ord(v) for v in labels], dtype=torch.float32)
+
+
+@pytest.mark.parametrize("k", [5, 3, 1])
+def test_int_small_kernels_vs_oracle(k):
+    """k < 7 (no golden holds one): the f32 cell at 1e-3 against the oracle,
+    and the bf16 cell (fused forward, banded backward convs with their
+    pre-loaded addends) within the bf16 golden bounds: logits 2e-2, gradient
+    cosine > 0.99 per tensor."""
+    from models import InT
+    x, y = _batch(60 + k, 3, 4)
+    m = _perturbed(InT.InT, 4, seed=k, k=k)
+    _vs_oracle(m, x, y)
+    from oracle import cells
+    dev = _dev()
+    sd = {n: v.detach().cpu().clone().requires_grad_(n != "unit1.w") for n, v in m.named_parameters()}
+    lo, _, _ = cells.recurrent_forward(sd, x)
+    cells.bce_logits(lo, y).backward()
+    m.zero_grad(set_to_none=True)
+    m.cell_dtype = "bf16"
+    out, _ = m(x.to(dev))
+    F.binary_cross_entropy_with_logits(out, y.to(dev).reshape(-1, 1)).backward()
+    _close("bf16 logits", out, lo, 2e-2)
+    for n, p in m.named_parameters():
+        if p.grad is None or sd[n].grad is None or sd[n].grad.norm() < 1e-8:
+            continue
+        a, b = p.grad.detach().cpu().double().flatten(), sd[n].grad.double().flatten()
+        cos = float(a @ b / (a.norm() * b.norm() + 1e-30))
+        assert cos > 0.99, f"bf16 {n}: cosine {cos:.4f}"
+
+
+def test_int_large_batch_bf16_vs_f32():
+    """B = 520 clips (past the 256 / 512 workgroups of one dispatch round, not
+    a multiple of 8 clips per XCD): the bf16 cell against the f32 cell on the
+    same clips -- logits within 2e-2, gradient cosine > 0.99 per tensor -- and
+    the bf16 step bitwise reproducible."""
+    from models import InT
+    dev = _dev()
+    x, y = _batch(91, 520, 6)
+    x, y = x.to(dev), y.to(dev)
+    m = _perturbed(InT.InT, 6, seed=17).to(dev)
+
+    def run(dtype):
+        m.cell_dtype = dtype
+        m.zero_grad(set_to_none=True)
+        out, _ = m(x)
+        F.binary_cross_entropy_with_logits(out, y.reshape(-1, 1)).backward()
+        return out.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()
+                                      if p.grad is not None}
+    o32, g32 = run("f32")
+    o16, g16 = run("bf16")
+    o16b, g16b = run("bf16")
+    assert torch.equal(o16, o16b) and all(torch.equal(g16[n], g16b[n]) for n in g16)
+    _close("bf16 logits", o16, o32, 2e-2)
+    for n in g32:
+        a, b = g16[n].double().flatten(), g32[n].double().flatten()
+        if b.norm() < 1e-8:
+            continue
+        cos = float(a @ b / (a.norm() * b.norm() + 1e-30))
+        assert cos > 0.99, f"{n}: cosine {cos:.4f}"
 
 
 @pytest.mark.parametrize("b,t", [(1, 1), (3, 2), (2, 1)])

@@ -147,14 +147,16 @@ def test_fused_forward_on_tiled_frames_is_bitwise_the_split_forward(cell, h, w, 
     assert not bad, bad
 
 
-@pytest.mark.parametrize("cell,k", [("int", 5), ("int", 3), ("int", 1), ("hgru", 5)])
-def test_banded_backward_convs_at_small_kernels_are_bitwise_the_whole_clip_conv(cell, k):
+@pytest.mark.parametrize("cell,k,hw", [("int", 5, 32), ("int", 3, 32), ("int", 1, 32), ("hgru", 5, 32),
+                                        ("hgru", 5, 64)])
+def test_banded_backward_convs_at_small_kernels_are_bitwise_the_whole_clip_conv(cell, k, hw):
     """k < 7 through the banded backward convs (k_conv_bwd_band2 and the fused
     backward A, whose addends are pre-loaded PT_BAND_LEAD tile-row steps
     ahead in the last kernel column: r06 fix -- for k < lead + 2 the first
     rows' pre-loads fell before the column's first step and were never
     issued) against the whole-clip k_conv_bwd (no pre-load) with the split
-    k_pw_ba; the forward through the fused segments at the same k."""
+    k_pw_ba; and the fused forward against the split one at the same k (64 x
+    64: the tiled frames' halos at k = 5)."""
     from models import InT, ffhgru_hierarchy as hg
     dev = _dev()
     torch.manual_seed(k + 11)
@@ -168,15 +170,18 @@ def test_banded_backward_convs_at_small_kernels_are_bitwise_the_whole_clip_conv(
                 p.uniform_(-0.5, 0.5)
     m = m.to(dev)
     m.cell_dtype = "bf16"
-    x = torch.rand(24, 3, 6, 32, 32, device=dev)
-    y = (torch.arange(24, device=dev) % 2).float()
+    x = torch.rand(24 if hw == 32 else 4, 3, 6, hw, hw, device=dev)
+    y = (torch.arange(x.shape[0], device=dev) % 2).float()
     o1, s1, g1, gr1 = _run(m, x, y, fused=True)                      # band2 + k_conv_pw_ba
-    o0, s0, g0, gr0 = _run(m, x, y, fused=True, band=0, cpa=0)       # k_conv_bwd + k_pw_ba
     assert torch.isfinite(o1).all()
-    assert torch.equal(o1, o0)
-    bad = {k2: ((gr1[k2] - gr0[k2]).abs().max() / gr0[k2].abs().max().clamp_min(1e-30)).item()
-           for k2 in gr0 if k2.startswith(("unit1.", "preproc.")) and not torch.equal(gr1[k2], gr0[k2])}
-    assert not bad, bad
+    for other in (dict(fused=True, band=0, cpa=0),                   # k_conv_bwd + k_pw_ba
+                  dict(fused=False, band=0, cpa=0)):                 # and the split forward
+        o0, s0, g0, gr0 = _run(m, x, y, **other)
+        for name, u, v in (("logits", o1, o0), ("states", s1, s0), ("gates", g1, g0)):
+            assert torch.equal(u, v), (other, name, (u - v).abs().max().item())
+        bad = {k2: ((gr1[k2] - gr0[k2]).abs().max() / gr0[k2].abs().max().clamp_min(1e-30)).item()
+               for k2 in gr0 if k2.startswith(("unit1.", "preproc.")) and not torch.equal(gr1[k2], gr0[k2])}
+        assert not bad, (other, bad)
 
 
 def _compare(cell, act, b, t, other):
