@@ -1,7 +1,10 @@
 """Edge cases and size-independent properties of the HIP cell (InT / hGRU).
 
 * smallest shapes against the CPU oracle (f32, 1e-3): one clip, one frame;
-  an odd batch with two frames; a single-clip 64x64 hGRU (tiles, B=1);
+  an odd batch with two frames; a single-clip 64x64 hGRU (tiles, B=1); the
+  same shapes through the bf16 path (logits 2e-2, gradient cosine > 0.99,
+  r06); kernel sizes 5, 3, 1 (no golden holds one) in f32 and bf16;
+* a 520-clip batch (more than one dispatch round) bf16 against f32;
 * raw u8 clips [B,T,H,W,3] as the cell input (PT_X_U8_NTHWC) against the
   f32 tensor engine.prepare_data builds from them: same values, so the cell's
   outputs and gradients agree bit for bit (InT f32 / bf16, tiled hGRU);
@@ -77,11 +80,18 @@ def test_int_small_kernels_vs_oracle(k):
     x, y = _batch(60 + k, 3, 4)
     m = _perturbed(InT.InT, 4, seed=k, k=k)
     _vs_oracle(m, x, y)
+    _vs_oracle_bf16(m, x, y)
+
+
+def _vs_oracle_bf16(m, x, y, hgru=False):
+    """The bf16 cell against the oracle within the bf16 golden bounds: logits
+    2e-2, gradient cosine > 0.99 per tensor with a non-trivial gradient."""
     from oracle import cells
     dev = _dev()
     sd = {n: v.detach().cpu().clone().requires_grad_(n != "unit1.w") for n, v in m.named_parameters()}
-    lo, _, _ = cells.recurrent_forward(sd, x)
+    lo, _, _ = cells.recurrent_forward(sd, x, hgru=hgru)
     cells.bce_logits(lo, y).backward()
+    m = m.to(dev)
     m.zero_grad(set_to_none=True)
     m.cell_dtype = "bf16"
     out, _ = m(x.to(dev))
@@ -133,10 +143,20 @@ def test_int_smallest_shapes(b, t):
     _vs_oracle(_perturbed(InT.InT, t, seed=b * 10 + t), x, y)
 
 
+@pytest.mark.parametrize("b,t", [(1, 1), (3, 2), (2, 3)])
+def test_int_smallest_shapes_bf16(b, t):
+    """The bf16 path (fused forward, the fused backward A from frame 1, the
+    first / last frame's k_pw_ba) at one and two frames."""
+    from models import InT
+    x, y = _batch(40 + b + t, b, t)
+    _vs_oracle_bf16(_perturbed(InT.InT, t, seed=b * 10 + t + 1), x, y)
+
+
 def test_hgru_single_clip_tiled():
     from models import ffhgru_hierarchy as hg
     x, y = _batch(31, 1, 3, hw=64)
     _vs_oracle(_perturbed(hg.FFhGRU, 3, seed=5), x, y, hgru=True)
+    _vs_oracle_bf16(_perturbed(hg.FFhGRU, 3, seed=5), x, y, hgru=True)
 
 
 @pytest.mark.parametrize("cell,dtype,hw", [("int", "f32", 32), ("int", "bf16", 32),
