@@ -152,8 +152,10 @@ def test_convlstm_jacobian_penalty_bf16_vs_f32():
     assert rel(o16, o32) < 1e-2, rel(o16, o32)
 
 
-def test_convlstm_bf16_tolerance():
-    """bf16 operands / saved h, f32 gate math and accumulation, k=15: outputs
+@pytest.mark.parametrize("tag", ["convlstm_k15", "convlstm_k7", "convlstm_t2"])
+def test_convlstm_bf16_tolerance(tag):
+    """bf16 operands / saved h, f32 gate math and accumulation, k=15 (and r06:
+    the k=7 prefetching loops, and the two-step unroll): outputs
     (after the batch-statistics BN, which amplifies h's rounding) within 1 %
     relative RMS of the reference; gradient cosine > 0.999 per tensor.  Until
     r05 the static x-conv (xg = Wx x + b, once per forward) ran with bf16 x and
@@ -166,7 +168,7 @@ def test_convlstm_bf16_tolerance():
     near f32; r06 computes it in three bf16 passes (hi x hi + lo x hi + hi x
     lo).  Measured values recorded (gpurun_out/parity_records.json)."""
     dev = _dev()
-    g = load("convlstm_k15")
+    g = load(tag)
     m = _model(g, "bf16").to(dev).train()
     img = torch.from_numpy(g["img"]).to(dev)
     tgt = torch.from_numpy(g["target"]).to(dev)
@@ -184,8 +186,8 @@ def test_convlstm_bf16_tolerance():
         a = p.grad.detach().cpu().double().flatten()
         cos[k] = float(a @ b / (a.norm() * b.norm() + 1e-30))
     from goldens import record
-    record("convlstm_k15_bf16_vs_reference", {"output_rel_rms": rel, "min_grad_cos": min(cos.values()),
-                                              "min_grad_cos_tensor": min(cos, key=cos.get)})
+    record(f"{tag}_bf16_vs_reference", {"output_rel_rms": rel, "min_grad_cos": min(cos.values()),
+                                         "min_grad_cos_tensor": min(cos, key=cos.get)})
     bad = {k: round(v, 6) for k, v in cos.items() if v <= 0.999}
     assert not bad, f"gradient cosine <= 0.999: {bad} (all: {cos})"
 
