@@ -10,7 +10,7 @@ ptamd.dist.CellDist, against the single-process HIP cell.
   segments, which read the all-rank totals through bnf_src; the banded
   backward convs).  bf16 tolerance: the two-rank totals are the same fp64
   sums in another association, so a bf16-stored value may round the other
-  way.
+  way.  r06: also the tiled hGRU (64 x 64, BatchNorm over clips x tiles).
 * early-gradient overlap: with per-replica BatchNorm (the default) the
   gradients averaged in two parts -- the cell's early gradients on a side
   stream behind the event the backward records before its k x k
@@ -39,10 +39,11 @@ def _free_port():
     return p
 
 
-def _model():
-    from models import InT
+def _model(tiled=False):
+    from models import InT, ffhgru_hierarchy as hg
     torch.manual_seed(21)
-    m = InT.InT(dimensions=32, timesteps=6, kernel_size=7)
+    m = (hg.FFhGRU(dimensions=32, timesteps=4, kernel_size=7) if tiled
+         else InT.InT(dimensions=32, timesteps=6, kernel_size=7))
     with torch.no_grad():
         for n, p in m.named_parameters():
             if (n.startswith("unit1.bn") and n.endswith("weight")) or n.endswith(("alpha", "kappa")):
@@ -52,14 +53,14 @@ def _model():
     return m
 
 
-def _batch():
+def _batch(tiled=False):
     from ptamd import synth
-    clips, labels = synth.make_batch(5, 4, 6)
+    clips, labels = (synth.make_batch(5, 4, 4, h=64, w=64) if tiled else synth.make_batch(5, 4, 6))
     x = torch.from_numpy(clips.transpose(0, 4, 1, 2, 3) / 255.0).float()
     return x, torch.tensor([ord(v) for v in labels], dtype=torch.float32)
 
 
-def _worker(rank, world, port, sync_bn, out_q, dtype="f32", three_part=True):
+def _worker(rank, world, port, sync_bn, out_q, dtype="f32", three_part=True, tiled=False):
     import sys
     sys.path[:0] = [os.path.join(REPO, "tests"), REPO, os.path.join(REPO, "pathtracker-models_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -68,9 +69,9 @@ def _worker(rank, world, port, sync_bn, out_q, dtype="f32", three_part=True):
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    m = _model().to(dev)
+    m = _model(tiled).to(dev)
     m.cell_dtype = dtype
-    x, y = _batch()
+    x, y = _batch(tiled)
     sh = slice(2 * rank, 2 * rank + 2)
     bucket = GradBucket(m.parameters(), dev, three_part=three_part)
     m.cell_dist = CellDist(sync_bn=sync_bn, bucket=bucket)
@@ -86,12 +87,13 @@ def _worker(rank, world, port, sync_bn, out_q, dtype="f32", three_part=True):
     dist.destroy_process_group()
 
 
-def _run_ranks(sync_bn, dtype="f32", three_part=True):
+def _run_ranks(sync_bn, dtype="f32", three_part=True, tiled=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, sync_bn, q, dtype, three_part)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sync_bn, q, dtype, three_part, tiled))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = {r: rest for r, *rest in (q.get(timeout=200) for _ in range(2))}
@@ -101,9 +103,9 @@ def _run_ranks(sync_bn, dtype="f32", three_part=True):
     return res
 
 
-def _single(x, y, dtype="f32"):
+def _single(x, y, dtype="f32", tiled=False):
     dev = torch.device("cuda:0")
-    m = _model().to(dev)
+    m = _model(tiled).to(dev)
     m.cell_dtype = dtype
     out, _ = m(x.to(dev))
     F.binary_cross_entropy_with_logits(out, y.to(dev).reshape(-1, 1)).backward()
@@ -138,18 +140,22 @@ def _close_grads(got, ref, rel, min_cos=None, tag=None):
 # bf16 bounds from the measured worst case (r05: max relative error 3.4e-6,
 # gradient cosine 1 - 5e-12, logits equal to 1e-6): the fp64 BatchNorm sums
 # added in another order move a value by at most a rounding step
-@pytest.mark.parametrize("dtype,atol,rel,min_cos", [("f32", 1e-5, 1e-5, None), ("bf16", 1e-4, 2e-4, 0.99999)])
-def test_syncbn_two_ranks_equal_single_process(dtype, atol, rel, min_cos):
+@pytest.mark.parametrize("dtype,atol,rel,min_cos,tiled", [("f32", 1e-5, 1e-5, None, False),
+                                                         ("bf16", 1e-4, 2e-4, 0.99999, False),
+                                                         ("f32", 1e-5, 1e-5, None, True),
+                                                         ("bf16", 1e-4, 2e-4, 0.99999, True)])
+def test_syncbn_two_ranks_equal_single_process(dtype, atol, rel, min_cos, tiled):
+    """(r06: also the tiled hGRU at 64 x 64 -- BatchNorm over clips x tiles)"""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
-    res = _run_ranks(sync_bn=True, dtype=dtype)
-    x, y = _batch()
-    lo, g = _single(x, y, dtype)
+    res = _run_ranks(sync_bn=True, dtype=dtype, tiled=tiled)
+    x, y = _batch(tiled)
+    lo, g = _single(x, y, dtype, tiled)
     for r in (0, 1):
         logits, early, grads = res[r]
         torch.testing.assert_close(torch.from_numpy(logits), lo[2 * r:2 * r + 2], rtol=0, atol=atol)
         assert early > 0                                 # the side-stream part ran
-        _close_grads(grads, g, rel, min_cos, tag=f"syncbn_{dtype}_rank{r}")
+        _close_grads(grads, g, rel, min_cos, tag=f"syncbn_{dtype}{'_tiled' if tiled else ''}_rank{r}")
 
 
 @pytest.mark.timeout(300)
